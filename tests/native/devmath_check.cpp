@@ -1,0 +1,48 @@
+// Exhaustive host check of csrc/tpt_devmath.h's glibc replicas and RNG form
+// against this image's glibc (run by tests/test_devmath.py).
+// usage: devmath_check [stride]   (stride 1 = every float of each domain)
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include "../../toypathtracer-games101-assignment7_amd/csrc/tpt_devmath.h"
+using namespace tpt;
+int main(int argc, char** argv) {
+    uint32_t stride = argc > 1 ? (uint32_t)atol(argv[1]) : 1;
+    long bad = 0, n = 0;
+    uint32_t hi = f2u(6.2831855f);
+    for (uint32_t u = 0; u <= hi; u += stride) {
+        float x = u2f(u);
+        n++;
+        if (f2u(sinf(x)) != f2u(tpt_sinf(x))) bad++;
+        if (f2u(cosf(x)) != f2u(tpt_cosf(x))) bad++;
+    }
+    printf("sincos n=%ld bad=%ld\n", n, bad);
+    long bad2 = 0, n2 = 0;
+    for (uint32_t u = 0; u < 0x7f800000u; u += stride) {
+        float x = u2f(u);
+        n2++;
+        if (f2u(atanf(x)) != f2u(tpt_atanf(x))) bad2++;
+    }
+    printf("atanf n=%ld bad=%ld\n", n2, bad2);
+    long bad3 = 0, n3 = 0;
+    const float roughs[] = {0.81f, 0.002f, 0.01f, 0.2f, 0.09f, 1.0f};
+    for (float r : roughs)
+        for (uint32_t k = 0; k <= (1u << 24); k += stride) {
+            float d1 = (float)k / (float)(1u << 24);
+            float y = r * std::sqrt(d1), x = std::sqrt(1.0f - d1);
+            n3++;
+            if (f2u(std::atan2(y, x)) != f2u(tpt_atan2f(y, x))) bad3++;
+        }
+    printf("atan2f n=%ld bad=%ld\n", n3, bad3);
+    long bad4 = 0, n4 = 0;
+    for (uint64_t x = 0; x <= 0xffffffffull; x += stride) {
+        uint32_t s = (uint32_t)x;
+        // rng_float advances the state; reproduce the single-step value directly
+        float a = (float)((double)s / 4294967295.0);
+        float b = (float)((double)s * (1.0 / 4294967295.0));
+        n4++;
+        if (f2u(a) != f2u(b)) bad4++;
+    }
+    printf("rng n=%ld bad=%ld\n", n4, bad4);
+    return (bad || bad2 || bad3 || bad4) ? 1 : 0;
+}

@@ -1,0 +1,82 @@
+"""The C-ABI library loads and exports every symbol the public headers declare;
+host-side pieces (presets, flattening, film output) work without a GPU."""
+import os
+import re
+
+import numpy as np
+import pytest
+
+import pytpt
+from conftest import ROOT
+from oracle_bind import Oracle
+
+HEADERS = [os.path.join(ROOT, "include", h) for h in ("tpt.h", "tpt_host.h")]
+
+
+def declared_functions():
+    names = set()
+    for h in HEADERS:
+        txt = open(h).read()
+        txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+        for m in re.finditer(r"^[A-Za-z_][\w\s\*]*?\b(tpt_\w+)\s*\(", txt, flags=re.M):
+            names.add(m.group(1))
+    return names
+
+
+def test_library_exports_every_declared_symbol():
+    L = pytpt.lib()
+    names = declared_functions()
+    assert {"tpt_create", "tpt_render", "tpt_upload_scene", "tpt_render_pixels"} <= names
+    for n in sorted(names):
+        assert hasattr(L, n), n
+    assert set(pytpt.EXPORTS) == names
+
+
+def test_abi_version_and_camera():
+    L = pytpt.lib()
+    assert L.tpt_abi_version() == 1
+    o = Oracle("standard")
+    # CalculateScale(fov) (SceneRenderingHelper.cpp:12-14), host-side, bit-exact
+    for fov in (40.0, 60.0, 90.0, 17.5):
+        assert np.float32(L.tpt_camera_scale(fov)).view(np.uint32) == np.float32(
+            o.L.oracle_camera_scale(fov)).view(np.uint32)
+
+
+@pytest.mark.parametrize("name,nobj,ntri", [("standard", 6, 32), ("silver", 6, 32), ("refractive_ball", 7, 32),
+                                            ("occlusion", 7, 36), ("bunny", 5, 4968 + 6 + 2 + 2 + 2)])
+def test_presets(name, nobj, ntri):
+    p = pytpt.Preset(name)
+    d = p.desc.contents
+    assert (d.width, d.height) == (784, 784)
+    assert d.num_objects == nobj
+    assert d.num_vertices == 3 * ntri
+    assert abs(d.fov - 40.0) < 1e-12
+    assert list(d.eye) == [278.0, 278.0, -800.0]
+
+
+def test_unknown_preset():
+    with pytest.raises(ValueError):
+        pytpt.Preset("nope")
+
+
+def test_create_without_gpu_fails_cleanly():
+    import ctypes
+    h = ctypes.c_void_p()
+    rc = pytpt.lib().tpt_create(0, ctypes.byref(h))
+    assert rc in (pytpt.TPT_OK, pytpt.TPT_E_DEVICE)
+    if rc == pytpt.TPT_OK:
+        pytpt.lib().tpt_destroy(h)
+    assert pytpt.lib().tpt_create(10**6, ctypes.byref(h)) == pytpt.TPT_E_DEVICE
+
+
+def test_film_output(tmp_path):
+    rgb = np.random.default_rng(0).random((40, 56, 3)).astype(np.float32)
+    for ext in ("jpg", "ppm", "pfm"):
+        pytpt.save_image(rgb, str(tmp_path / ("x." + ext)))
+    data = (tmp_path / "x.jpg").read_bytes()
+    assert data[:2] == b"\xff\xd8" and data[-2:] == b"\xff\xd9"
+    ppm = (tmp_path / "x.ppm").read_bytes()
+    px = np.frombuffer(ppm[len(b"P6\n56 40\n255\n"):], np.uint8).reshape(40, 56, 3)
+    # SceneRenderingHelper.cpp:62-64
+    want = (255 * np.power(np.clip(rgb, 0, 1), np.float32(0.6))).astype(np.uint8)
+    assert np.abs(px.astype(int) - want.astype(int)).max() <= 1

@@ -1,0 +1,98 @@
+"""Pin the CPU restatement (oracle/tpt_oracle.cpp) against the reference.
+
+1. against the committed golden fixtures (made by tests/golden/make_golden.py from
+   the REAL reference build, oracle/_ref) -- bit-exact;
+2. live against oracle/_ref/libref.so on fresh inputs, where that library exists.
+"""
+import numpy as np
+import pytest
+
+from conftest import PRESETS, bits, golden
+from oracle_bind import Oracle, Reference, ref_available
+
+
+def eq_bits(a, b):
+    return np.array_equal(bits(a), bits(b))
+
+
+def test_rng_stream():
+    g = golden("rng.npz")
+    o = Oracle("standard")
+    for k, s in enumerate(g["seeds"]):
+        u, f = o.rng(int(s), g["u32"].shape[1])
+        assert np.array_equal(u, g["u32"][k])
+        assert eq_bits(f, g["f"][k])
+    # known answer quoted in SURVEY.md §8(c): seed 1 -> 268476417, 1157628417, ...
+    assert list(g["u32"][0][:4]) == [268476417, 1157628417, 1158709409, 269814307]
+
+
+def test_material_kat():
+    g = golden("kat_material.npz")
+    o = Oracle("standard")
+    for k, name in enumerate(g["names"]):
+        out = o.material_kat(g["mats"][k], g["cases"])
+        assert eq_bits(out, g["out"][k]), name
+
+
+def test_helper_kat():
+    g = golden("kat_helpers.npz")
+    assert eq_bits(Oracle("standard").helper_kat(g["cases"]), g["out"])
+
+
+@pytest.mark.parametrize("preset", PRESETS)
+def test_intersect(preset):
+    g = golden("intersect_%s.npz" % preset)
+    o = Oracle(preset)
+    for c in range(3):
+        assert eq_bits(o.intersect(g["rays"], c), g["hits"][c])
+
+
+@pytest.mark.parametrize("preset", PRESETS)
+def test_pixels_pt(preset):
+    g = golden("pixels_%s.npz" % preset)
+    o = Oracle(preset)
+    assert eq_bits(o.trace_pixels(0, 1, g["pix"])[0], g["pt1"])
+    assert eq_bits(o.trace_pixels(0, 16, g["pix"])[0], g["pt16"])
+
+
+@pytest.mark.parametrize("preset", PRESETS)
+def test_pixels_bdpt(preset):
+    g = golden("pixels_%s.npz" % preset)
+    o = Oracle(preset)
+    rgb, splat, b = o.trace_pixels(1, 4, g["bpix"], want_splat=True)
+    assert eq_bits(rgb, g["bdpt4"])
+    assert np.array_equal(b, g["bdpt4_bounces"])
+    flat = splat.reshape(-1)
+    assert np.array_equal(np.nonzero(flat)[0], g["splat_idx"])
+    assert eq_bits(flat[g["splat_idx"]], g["splat_val"])
+
+
+def test_full_image_pt():
+    g = golden("image_standard.npz")
+    img, _ = Oracle("standard").render(0, 16, threads=8)
+    blocks = img.reshape(98, 8, 98, 8, 3).astype(np.float64).mean((1, 3)).astype(np.float32)
+    assert eq_bits(blocks, g["pt16_blocks"])
+    y, x = g["crop_origin"]
+    assert eq_bits(img[y:y + 64, x:x + 64], g["pt16_crop"])
+
+
+def test_full_image_bdpt():
+    # Renderer::Render with -j1: splat buffers merged after the radiance (Renderer.cpp:98-114)
+    g = golden("image_standard.npz")
+    img, _ = Oracle("standard").render(1, 2, threads=1)
+    blocks = img.reshape(98, 8, 98, 8, 3).astype(np.float64).mean((1, 3)).astype(np.float32)
+    assert eq_bits(blocks, g["bdpt2_blocks"])
+    y, x = g["crop_origin"]
+    assert eq_bits(img[y:y + 64, x:x + 64], g["bdpt2_crop"])
+
+
+@pytest.mark.skipif(not ref_available(), reason="oracle/_ref/libref.so not built")
+@pytest.mark.parametrize("preset", PRESETS)
+def test_live_against_reference(preset):
+    rng = np.random.default_rng(hash(preset) % 2**32)
+    pix = np.sort(rng.choice(784 * 784, 3000, replace=False))
+    R, o = Reference(preset), Oracle(preset)
+    assert eq_bits(o.trace_pixels(0, 8, pix)[0], R.trace_pixels(0, 8, pix)[0])
+    a = o.trace_pixels(1, 2, pix[:400], want_splat=True)
+    b = R.trace_pixels(1, 2, pix[:400], want_splat=True)
+    assert eq_bits(a[0], b[0]) and eq_bits(a[1], b[1]) and np.array_equal(a[2], b[2])

@@ -1,0 +1,299 @@
+// tpt_bdpt.h -- bidirectional path tracing sample on gfx950 (BDPT.cpp:17-351,
+// BDPT.hpp:15-169), arithmetic-identical to the reference.
+//
+// GPU restructuring (results unchanged, see tests/test_gpu_parity.py):
+//  * BDPTPath::PathWeight (BDPT.cpp:173-259) copies a 3.6 KB path and re-Appends
+//    the other subpath vertex by vertex to obtain reverse pdfs.  Append only reads
+//    the appended vertex, the current last vertex and the one before it, and the
+//    throughput it computes is never read by PathWeight.  So the k-th appended
+//    vertex's pdf depends on the (s,t) connection only for k = 0, 1; for k >= 2 it
+//    is a function of one subpath alone and is computed once
+//    per path (`rev`), then multiplied by the same RR factor (count > 4 ? .8 : 1)
+//    and folded into the same sequential cur_pdf / weightdenominator chain with the
+//    same cur_pdf == 0 early exit.
+//  * FillPathUsingRussianRoulette (BDPT.cpp:92-118) draws the RR random number
+//    right after Material::sample; SampleNextVertex's intersection and BSDF
+//    evaluation draw nothing, so they are skipped when the RR draw ends the path
+//    and the BSDF evaluation is skipped when the pdf test ends it.
+//  * The camera vertex v1 is the same for every sample (no jitter) and is hoisted
+//    out of the spp loop.
+//  * t = 1 splats (DrawToImage, SceneRenderingHelper.cpp:30-55) are fp32 atomics;
+//    zero contributions are skipped (adding +-0 never changes an fp32 sum here).
+#pragma once
+
+#include "tpt_device.h"
+
+namespace tpt {
+
+constexpr int kMaxLen = 16;                   // MAX_BDPT_PATH_LENGTH (BDPT.hpp:8)
+constexpr float kCamZeroPdf = (float)1e10;    // CAMERA_ZERO_PDF (BDPT.cpp:7)
+constexpr float kCamRayPdf = (float)10.0;     // CAMERA_RAY_PDF (BDPT.cpp:8)
+
+// BDPTPath::InternalPathVertex (BDPT.hpp:16-21) + cached reverse pdf.
+struct BVert {
+    V3 x, N;
+    int type, prim;
+    float pdf;
+    V3 alpha;
+    float rev;
+};
+
+TPT_D PTV as_ptv(const BVert& b) {
+    PTV v;
+    v.x = b.x; v.N = b.N; v.type = b.type; v.prim = b.prim;
+    return v;
+}
+TPT_D V3 normal_of(int type, V3 N) { return type == T_CAM ? v3(0.0f, 0.0f, 1.0f) : N; }  // BDPT.hpp:91-95
+
+// SrpdfToAreaPdf (SampleHelperFunctions.hpp:122-131)
+TPT_D float srpdf_to_area(float sr, int t1, V3 x1, V3 n1, int t2, V3 x2, V3 n2) {
+    float d2;
+    V3 w = normalize_len2(x2 - x1, &d2);
+    float c1 = t1 == T_CAM ? 1.0f : (float)dabs_(dot3(w, n1));
+    float c2 = t2 == T_CAM ? 1.0f : (float)dabs_(dot3(-w, n2));
+    return sr * fabs_(c1 * c2 / d2);
+}
+
+// PathVertex::EvalPdfOnSolidAngle (BDPT.cpp:332-351); `pre` = Pre().Position()
+TPT_D float eval_pdf_sa(const DScene& s, int type, int prim, V3 x, V3 N, V3 pre, V3 dir) {
+    const V3 n = normal_of(type, N);
+    float c = (float)dabs_(dot3(dir, n));
+    if (type == T_LIGHT) return safe_div(cosine_pdf(n, dir), c);
+    if (type == T_CAM) return kCamRayPdf;
+    if (c == 0.0f) return 0.0f;
+    V3 wo = normalized(pre - x);
+    return safe_div(mat_pdf(load_mat(s, prim_mat(s, prim)), wo, n, dir), c);
+}
+// PathVertex::EvalBsdfOnSolidAngle (BDPT.cpp:317-330)
+TPT_D V3 eval_bsdf_sa(const DScene& s, int type, int prim, V3 x, V3 N, V3 pre, V3 dir) {
+    if (type == T_LIGHT || type == T_CAM) return v3s(1.0f);
+    return eval_bsdf(load_mat(s, prim_mat(s, prim)), normalized(pre - x), dir, normal_of(type, N), false);
+}
+// Append's pdf for `v` appended after `last` (whose predecessor is at `pre`), before
+// the RR factor (BDPT.cpp:154-158).
+TPT_D float append_pdf(const DScene& s, int ltype, int lprim, V3 lx, V3 lN, V3 pre, int vtype, V3 vx, V3 vN) {
+    float d2;
+    V3 wi = normalize_len2(vx - lx, &d2);
+    float sr = eval_pdf_sa(s, ltype, lprim, lx, lN, pre, wi);
+    return srpdf_to_area(sr, ltype, lx, lN, vtype, vx, vN);
+}
+TPT_D float rr_of(int count) { return count > 4 ? .8f : 1.f; }
+
+// Object::pdf() of a primitive (Triangle::pdf / Sphere::pdf), for Append(count==0)
+TPT_D float prim_pdf(const DScene& s, int prim) {
+    return prim < s.ntri ? 1.0f / s.trix[prim].area : 1.0f / s.sph[prim - s.ntri].area;
+}
+
+// Scene::ShadowCheck(const PTVertex&, const PTVertex&) (Scene.cpp:50-83)
+TPT_D bool shadow_v(const DScene& s, const BVert& v1, const BVert& v2, int* stk) {
+    V3 atob = v2.x - v1.x;
+    if (v1.prim >= 0 && v2.prim != v1.prim && s.mats[prim_mat(s, v1.prim)].type == TPT_TRANSPARENT) {
+        if (dot3(atob, v1.N) < 0.0f) return shadow_pts(s, v1.x, v2.x, TPT_CULL_FRONT, stk);
+        return shadow_pts(s, v1.x, v2.x, TPT_CULL_BACK, stk);
+    }
+    if (v1.prim >= 0 && dot3(atob, v1.N) < 0.0f) return false;
+    if (v2.prim >= 0 && dot3(-atob, v2.N) < 0.0f) return false;
+    return shadow_pts(s, v1.x, v2.x, TPT_CULL_BACK, stk);
+}
+
+// FillPathUsingRussianRoulette (BDPT.cpp:92-118) + SampleNextVertex (:261-279).
+TPT_D int fill_path(const DScene& s, BVert* P, int start, uint32_t& rs, int* stk) {
+    int count = start + 1;
+    for (int i = start; i < kMaxLen - 1; i++) {
+        BVert cur = P[i];
+        if (cur.type == T_BG) break;
+        V3 wo = normalized(P[i - 1].x - cur.x);
+        const Mat m = load_mat(s, prim_mat(s, cur.prim));
+        float raw;
+        V3 wi = mat_sample(m, wo, cur.N, &raw, rs);
+        const float rr = i > 4 ? .8f : 1.f;
+        if (rng_float(rs) > rr) break;
+        float ct = (float)dabs_(dot3(cur.N, wi));
+        float sr = safe_div(raw, ct);
+        PTV it = scene_intersect(s, make_ray(cur.x, wi), dot3(cur.N, wi) > 0.0f ? TPT_CULL_BACK : TPT_CULL_FRONT, stk);
+        float pdf = srpdf_to_area(sr, cur.type, cur.x, cur.N, it.type, it.x, it.N);
+        if (pdf == 0.0f) break;
+        V3 bsdf = eval_bsdf(m, wo, wi, cur.N, false);
+        BVert nx;
+        nx.x = it.x; nx.N = it.N; nx.type = it.type; nx.prim = it.prim;
+        nx.pdf = pdf * rr;
+        nx.alpha = divs(cur.alpha * safe_div(bsdf, sr), rr);
+        nx.rev = 0.0f;
+        P[i + 1] = nx;
+        count++;
+    }
+    return count;
+}
+
+// Reverse pdfs of vertices j = 0..count-3 (Append with last = j+1, Pre = j+2).
+TPT_D void path_rev(const DScene& s, BVert* P, int count) {
+    for (int j = 0; j + 2 < count; ++j) {
+        const BVert& a = P[j + 1];
+        P[j].rev = append_pdf(s, a.type, a.prim, a.x, a.N, P[j + 2].x, P[j].type, P[j].x, P[j].N);
+    }
+}
+
+// BDPTPath::PathWeight (BDPT.cpp:173-259) for light sub-length sl, camera sub-length tl.
+TPT_D V3 path_weight(const DScene& s, const BVert* L, int sl, const BVert* C, int tl, int* stk) {
+    const int z = tl - 1;
+    const BVert cz = C[z];
+    if (cz.type == T_BG) return sl == 0 ? cz.alpha * v3(s.bg[0], s.bg[1], s.bg[2]) : v3s(0.0f);
+    if (sl != 0 && L[sl - 1].type == T_BG) return v3s(0.0f);
+    V3 cst;
+    if (sl == 0) {
+        V3 wi = normalized(C[z - 1].x - cz.x);
+        V3 em = v3s(0.0f);  // PathVertex::Emission (BDPT.hpp:119-128)
+        if (cz.prim >= 0) em = load_mat(s, prim_mat(s, cz.prim)).em;
+        cst = mul(em, (float)dot3(normal_of(cz.type, cz.N), wi));
+        if (dot3(em, em) == 0.0f) return v3s(0.0f);
+    } else {
+        const BVert ly = L[sl - 1];
+        float d2;
+        V3 dir = normalize_len2(cz.x - ly.x, &d2);
+        if (shadow_v(s, cz, ly, stk)) return v3s(0.0f);
+        V3 fl = eval_bsdf_sa(s, ly.type, ly.prim, ly.x, ly.N, sl >= 2 ? L[sl - 2].x : ly.x, dir);
+        V3 fc = eval_bsdf_sa(s, cz.type, cz.prim, cz.x, cz.N, z >= 1 ? C[z - 1].x : cz.x, -dir);
+        cst = mul(fl * fc, (float)dabs_(dot3(normal_of(ly.type, ly.N), dir) * dot3(normal_of(cz.type, cz.N), -dir) / (double)d2));
+    }
+    float wd = 1.0f;
+    // loop A: camera prefix C[0..tl), append L[sl-1], ..., L[0]
+    float cur = 1.0f;
+    for (int k = 0; k < sl; ++k) {
+        const int j = sl - 1 - k;
+        const BVert v = L[j];
+        float pdf;
+        if (k == 0) pdf = append_pdf(s, cz.type, cz.prim, cz.x, cz.N, z >= 1 ? C[z - 1].x : cz.x, v.type, v.x, v.N);
+        else if (k == 1) {
+            const BVert a = L[sl - 1];
+            pdf = append_pdf(s, a.type, a.prim, a.x, a.N, cz.x, v.type, v.x, v.N);
+        } else pdf = v.rev;
+        pdf *= rr_of(tl + k);
+        cur *= safe_div(pdf, v.pdf);
+        wd += cur * cur;
+        if (cur == 0.0f) break;
+    }
+    // loop B: light prefix L[0..sl), append C[tl-1], ..., C[0]
+    cur = 1.0f;
+    for (int k = 0; k < tl; ++k) {
+        const int j = tl - 1 - k;
+        const BVert v = C[j];
+        const int count = sl + k;
+        float pdf;
+        if (count == 0) {
+            pdf = prim_pdf(s, v.prim);  // Append(count==0): vertex.obj->pdf(), no RR factor
+        } else {
+            if (k == 0) {
+                const BVert a = L[sl - 1];
+                pdf = append_pdf(s, a.type, a.prim, a.x, a.N, sl >= 2 ? L[sl - 2].x : a.x, v.type, v.x, v.N);
+            } else if (k == 1) {
+                // last = C[tl-1] as appended (type Light when it opened the path, BDPT.cpp:240-242)
+                const int at = sl == 0 ? T_LIGHT : cz.type;
+                pdf = append_pdf(s, at, cz.prim, cz.x, cz.N, sl >= 1 ? L[sl - 1].x : cz.x, v.type, v.x, v.N);
+            } else {
+                pdf = v.rev;
+            }
+            pdf *= rr_of(count);
+        }
+        cur *= safe_div(pdf, v.pdf);
+        wd += cur * cur;
+        if (cur == 0.0f) break;
+    }
+    V3 lt = sl == 0 ? v3s(1.0f) : L[sl - 1].alpha;
+    V3 uc = lt * cz.alpha * cst;
+    return divs(uc, wd);
+}
+
+// DrawToImage (SceneRenderingHelper.cpp:24-55), BlendMode::Additive, fp32 atomics.
+TPT_D void splat_add(const DScene& s, V3 light, V3 cam, V3 value, float* splat) {
+    if (value.x == 0.0f && value.y == 0.0f && value.z == 0.0f) return;
+    V3 d = normalized(light - cam);
+    d = divs(d, d.z);
+    float aspect = (float)(s.width / s.height);
+    V3 t = v3(-d.x / s.scale / aspect, -d.y / s.scale, 0.0f);
+    V3 uv = mul(t + v3s(1.0f), 0.5f);
+    float cx = uv.x * s.width, cy = uv.y * s.height;
+    int ix0 = (int)cx, iy0 = (int)cy;
+    for (int ix = ix0 - 1; ix <= ix0 + 1; ix++)
+        for (int iy = iy0 - 1; iy <= iy0 + 1; iy++) {
+            if (ix < 0 || iy < 0 || ix >= s.width || iy >= s.height) continue;
+            float dx = fabs_(cx - (ix + 0.5f)), dy = fabs_(cy - (iy + 0.5f));
+            float w = smax(0.0f, 1.0f - dx) * smax(0.0f, 1.0f - dy);
+            V3 c = mul(value, w);
+            float* b = splat + 3 * ((int64_t)ix + (int64_t)s.height * iy);
+            if (c.x != 0.0f) atomicAdd(b + 0, c.x);
+            if (c.y != 0.0f) atomicAdd(b + 1, c.y);
+            if (c.z != 0.0f) atomicAdd(b + 2, c.z);
+        }
+}
+
+// One pixel stream: Renderer.cpp:42-52 with BDPT (BDPT.cpp:282-315).
+TPT_D void bdpt_pixel(const DScene& s, int64_t i, int spp, V3& acc, float* splat, unsigned long long& nbounce,
+                      int* stk) {
+    BVert C[kMaxLen], L[kMaxLen];
+    const int px = (int)(i % s.width), py = (int)(i / s.width);
+    const V3 dir = pixel_ray(px, py, s.width, s.height, s.scale);
+    const V3 eye = v3(s.eye[0], s.eye[1], s.eye[2]);
+    const Ray cray = make_ray(eye, dir);
+    // GenerateCameraPath (BDPT.cpp:41-59): v0, v1 identical for every sample
+    BVert c0;
+    c0.x = eye; c0.N = v3s(0.0f); c0.type = T_CAM; c0.prim = -1;
+    c0.pdf = kCamZeroPdf; c0.alpha = v3s(1.0f); c0.rev = 0.0f;
+    PTV h1 = scene_intersect(s, cray, TPT_CULL_BACK, stk);
+    BVert c1;
+    c1.x = h1.x; c1.N = h1.N; c1.type = h1.type; c1.prim = h1.prim;
+    c1.pdf = srpdf_to_area(kCamRayPdf, T_CAM, c0.x, c0.N, h1.type, h1.x, h1.N);
+    c1.alpha = v3s(1.0f);
+    c1.rev = 0.0f;
+    const DObj lo = s.objs[s.emitters[0]];
+    const V3 lem = load_mat(s, lo.mat).em;
+    const float inv = 1.0f / spp;
+    uint32_t rs = (uint32_t)((int)i + 1);
+    acc = v3s(0.0f);
+    for (int sp = 0; sp < spp; ++sp) {
+        C[0] = c0;
+        C[1] = c1;
+        int cn = 2;
+        if (c1.type != T_BG) cn = fill_path(s, C, 1, rs, stk);
+        // GenerateLightPath (BDPT.cpp:61-90) from m_emissionObjects[0]
+        int ln;
+        {
+            V3 pc, pn;
+            int pp;
+            object_sample(s, lo, pc, pn, pp, rs);
+            BVert l0;
+            l0.x = pc; l0.N = pn; l0.type = T_LIGHT; l0.prim = pp;
+            l0.pdf = lo.pdf;
+            l0.alpha = divs(lem, l0.pdf);
+            l0.rev = 0.0f;
+            float pdf1;
+            V3 wi = cosine_sample(pn, pdf1, rs);
+            float ct = (float)dot3(l0.N, wi);
+            pdf1 = safe_div(pdf1, ct);
+            PTV it = scene_intersect(s, make_ray(l0.x, wi), TPT_CULL_BACK, stk);
+            BVert l1;
+            l1.x = it.x; l1.N = it.N; l1.type = it.type; l1.prim = it.prim;
+            l1.pdf = srpdf_to_area(pdf1, T_LIGHT, l0.x, l0.N, it.type, it.x, it.N);
+            l1.alpha = v3s(0.0f);  // fresh InternalPathVertex (BDPT.hpp:19)
+            l1.rev = 0.0f;
+            L[0] = l0;
+            if (pdf1 != 0.0f) l1.alpha = safe_div(l0.alpha, pdf1);
+            L[1] = l1;
+            if (pdf1 == 0.0f && it.type == T_BG) ln = 2;
+            else ln = fill_path(s, L, 1, rs, stk);
+        }
+        nbounce += (unsigned long long)(cn + ln);
+        path_rev(s, C, cn);
+        path_rev(s, L, ln);
+        V3 res = v3s(0.0f);
+        for (int t = 1; t <= cn; ++t)
+            for (int sl = 0; sl <= ln; ++sl) {
+                if (t + sl < 2) continue;
+                V3 w = vmax0(path_weight(s, L, sl, C, t, stk));
+                if (t > 1) res = res + w;
+                else if (splat) splat_add(s, L[sl - 1].x, C[0].x, w, splat);
+            }
+        acc = acc + mul(res, inv);
+    }
+}
+
+}  // namespace tpt

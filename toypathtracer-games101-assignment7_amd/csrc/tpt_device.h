@@ -1,0 +1,589 @@
+// tpt_device.h -- gfx950 device code of the hot path: BVH traversal, primitive
+// tests, GGX/Lambert/Fresnel BSDF, light sampling, the PT sample and the BDPT
+// sample.  Every function cites the reference code it reproduces; arithmetic
+// follows the numerics contract of tpt_devmath.h (kernels are built with
+// -ffp-contract=off).
+//
+// Memory model: the scene (tpt_scene.h) is read through the L1/L2 (it is a few KB
+// for the Cornell presets, <1 MB with the bunny); the per-lane BVH stack lives in
+// LDS in a [depth][lane] layout so that ds_read/ds_write_b32 from a wave never
+// bank-conflict (bank = lane mod 32 whatever the per-lane depth).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "../../include/tpt.h"
+#include "tpt_devmath.h"
+#include "tpt_scene.h"
+
+namespace tpt {
+
+#define TPT_D __device__ __forceinline__
+
+constexpr int kBlock = 256;     // threads per workgroup (4 waves)
+constexpr int kStackCap = 32;   // LDS stack entries per lane (upload rejects deeper trees)
+
+// ------------------------------------------------------------------ rays --
+struct Ray {
+    V3 o, d, inv;
+};
+TPT_D Ray make_ray(V3 o, V3 d) {  // Ray.hpp:12-15
+    Ray r;
+    r.o = o;
+    r.d = d;
+    r.inv = v3((float)(1. / (double)d.x), (float)(1. / (double)d.y), (float)(1. / (double)d.z));
+    return r;
+}
+
+struct Hit {
+    double dist;
+    int prim;  // -1: no hit
+};
+
+// Bounds3::IntersectP (Bounds3.hpp:92-115): nmin starts at FLT_MIN, std::max /
+// std::min ignore a NaN second argument, hit iff nmax > 0 && nmin <= nmax.
+TPT_D bool box_hit(const DNode& n, const Ray& r) {
+    float nmin = 1.17549435e-38f, nmax = 3.40282347e+38f;
+    {
+        float t1 = (n.bmin[0] - r.o.x) * r.inv.x, t2 = (n.bmax[0] - r.o.x) * r.inv.x;
+        if (t1 > t2) { float t = t1; t1 = t2; t2 = t; }
+        nmin = smax(nmin, t1); nmax = smin(nmax, t2);
+    }
+    {
+        float t1 = (n.bmin[1] - r.o.y) * r.inv.y, t2 = (n.bmax[1] - r.o.y) * r.inv.y;
+        if (t1 > t2) { float t = t1; t1 = t2; t2 = t; }
+        nmin = smax(nmin, t1); nmax = smin(nmax, t2);
+    }
+    {
+        float t1 = (n.bmin[2] - r.o.z) * r.inv.z, t2 = (n.bmax[2] - r.o.z) * r.inv.z;
+        if (t1 > t2) { float t = t1; t1 = t2; t2 = t; }
+        nmin = smax(nmin, t1); nmax = smin(nmax, t2);
+    }
+    return nmax > 0.0f && nmin <= nmax;
+}
+
+TPT_D V3 tri_normal(const DTri& t) { return v3(t.nx, t.ny, t.nz); }
+
+// Triangle::GetIntersection (Triangle.cpp:77-118): culling on the f64 sign of
+// dot(d, n), then f64 Moller-Trumbore with |det| < EPSILON(1e-4f) rejection.
+TPT_D bool tri_test(const DTri& t, const Ray& r, int cull, double& dist) {
+    V3 n = tri_normal(t);
+    if (cull == TPT_CULL_BACK) {
+        if (dot3(r.d, n) > 0) return false;
+    } else if (cull == TPT_CULL_FRONT) {
+        if (dot3(r.d, n) < 0) return false;
+    }
+    V3 e1 = v3(t.e1[0], t.e1[1], t.e1[2]), e2 = v3(t.e2[0], t.e2[1], t.e2[2]);
+    V3 pvec = cross(r.d, e2);
+    double det = dot3(e1, pvec);
+    if (dabs_(det) < (double)1e-4f) return false;
+    double det_inv = 1. / det;
+    V3 tvec = r.o - v3(t.v0[0], t.v0[1], t.v0[2]);
+    double u = dot3(tvec, pvec) * det_inv;
+    if (u < 0 || u > 1) return false;
+    V3 qvec = cross(tvec, e1);
+    double v = dot3(r.d, qvec) * det_inv;
+    if (v < 0 || u + v > 1) return false;
+    double tt = dot3(e2, qvec) * det_inv;
+    if (tt < 0.0f) return false;
+    dist = tt;
+    return true;
+}
+
+// SolveQuadratic (SampleHelperFunctions.cpp:4-18), float parameters.
+TPT_D bool solve_quadratic(float a, float b, float c, float& x0, float& x1) {
+    double discr = (double)b * b - 4.0 * a * c;
+    if (discr < 0) return false;
+    if (discr == 0) {
+        x0 = x1 = (float)(-0.5 * b / a);
+    } else {
+        float q = (b > 0) ? (float)(-0.5 * (b + sqrt_d(discr))) : (float)(-0.5 * (b - sqrt_d(discr)));
+        x0 = q / a;
+        x1 = c / q;
+    }
+    if (x0 > x1) { float t = x0; x0 = x1; x1 = t; }
+    return true;
+}
+// Sphere::GetIntersection (Sphere.cpp:4-41)
+TPT_D bool sphere_test(const DSphere& s, const Ray& r, int cull, double& dist) {
+    V3 L = r.o - v3(s.c[0], s.c[1], s.c[2]);
+    double a = dot3(r.d, r.d);
+    double b = 2.0 * dot3(r.d, L);
+    double c = dot3(L, L) - s.r2;
+    float t0, t1;
+    if (!solve_quadratic((float)a, (float)b, (float)c, t0, t1)) return false;
+    float tk;
+    if (cull == TPT_CULL_BACK) tk = t0;
+    else if (cull == TPT_CULL_FRONT) tk = t1;
+    else tk = t0 <= 0 ? t1 : t0;
+    if (tk > 0.0f) { dist = tk; return true; }
+    return false;
+}
+
+// BVHAccel::Intersect (BVH.cpp:103-143) from `root`, both levels spliced
+// (tpt_scene.h).  Same pop order (right child first), strict `>` on the f64
+// distance, so ties resolve exactly as in the reference.
+TPT_D Hit traverse(const DScene& s, int root, const Ray& r, int cull, int* stk) {
+    Hit best;
+    best.prim = -1;
+    best.dist = 0.0;
+    if (root < 0) return best;
+    int sp = 0;
+    stk[0] = root;
+    sp = 1;
+    while (sp > 0) {
+        --sp;
+        const int ni = stk[sp * kBlock];
+        const DNode n = s.nodes[ni];
+        if (!box_hit(n, r)) continue;
+        if (n.a >= 0) {
+            stk[sp * kBlock] = n.a;
+            stk[(sp + 1) * kBlock] = n.b;
+            sp += 2;
+            continue;
+        }
+        if (n.a == kEmptyLeaf) continue;
+        const int prim = -1 - n.a;
+        double dist;
+        bool h;
+        if (prim < s.ntri) h = tri_test(s.tris[prim], r, cull, dist);
+        else h = sphere_test(s.sph[prim - s.ntri], r, cull, dist);
+        if (h && (best.prim < 0 || best.dist > dist)) {
+            best.dist = dist;
+            best.prim = prim;
+        }
+    }
+    return best;
+}
+
+// Intersection fields of a hit (Triangle.cpp:109-114, Sphere.cpp:30-36)
+TPT_D void hit_geometry(const DScene& s, const Ray& r, const Hit& h, V3& x, V3& n) {
+    if (h.prim < s.ntri) {
+        x = r.o + mul(r.d, (float)h.dist);
+        n = tri_normal(s.tris[h.prim]);
+    } else {
+        const DSphere& sp = s.sph[h.prim - s.ntri];
+        x = r.o + mul(r.d, (float)h.dist);
+        n = normalized(x - v3(sp.c[0], sp.c[1], sp.c[2]));
+    }
+}
+TPT_D int prim_mat(const DScene& s, int prim) {
+    return prim < s.ntri ? s.trix[prim].mat : s.sph[prim - s.ntri].mat;
+}
+
+// PTVertex (PTVertex.hpp:6-21).  prim = Object* of the reference (-1 = nullptr).
+enum { T_BG = 0, T_MID = 1, T_LIGHT = 2, T_CAM = 3 };
+struct PTV {
+    V3 x, N;
+    int type;
+    int prim;
+};
+TPT_D PTV ptv_bg() {
+    PTV v;
+    v.x = v3s(0.0f);
+    v.N = v3s(0.0f);
+    v.type = T_BG;
+    v.prim = -1;
+    return v;
+}
+// Scene::Intersect (Scene.cpp:21-35)
+TPT_D PTV scene_intersect(const DScene& s, const Ray& r, int cull, int* stk) {
+    Hit h = traverse(s, 0, r, cull, stk);
+    PTV v = ptv_bg();
+    if (h.prim >= 0) {
+        hit_geometry(s, r, h, v.x, v.N);
+        v.type = T_MID;
+        v.prim = h.prim;
+    }
+    return v;
+}
+// Scene::ShadowCheck(Vector3f, Vector3f, FaceCulling) (Scene.cpp:37-48)
+TPT_D bool shadow_pts(const DScene& s, V3 lc, V3 x, int cull, int* stk) {
+    double ld2 = dot3(lc - x, lc - x);
+    Ray r = make_ray(lc, normalized(x - lc));
+    Hit h = traverse(s, 0, r, cull, stk);
+    if (h.prim < 0) return false;
+    V3 hx, hn;
+    hit_geometry(s, r, h, hx, hn);
+    double sd2 = dot3(hx - lc, hx - lc);
+    return sd2 < ld2 - 1.0f;
+}
+
+// ------------------------------------------------------------ materials --
+struct Mat {
+    int type;
+    V3 em, ior_m, ior_m_k, kd;
+    float ior_d, rough;
+};
+TPT_D Mat load_mat(const DScene& s, int mi) {
+    const DMat& m = s.mats[mi];
+    Mat r;
+    r.type = m.type;
+    r.em = v3(m.em[0], m.em[1], m.em[2]);
+    r.ior_m = v3(m.ior_m[0], m.ior_m[1], m.ior_m[2]);
+    r.ior_m_k = v3(m.ior_m_k[0], m.ior_m_k[1], m.ior_m_k[2]);
+    r.kd = v3(m.kd[0], m.kd[1], m.kd[2]);
+    r.ior_d = m.ior_d;
+    r.rough = m.rough;
+    return r;
+}
+
+TPT_D float saturate(float t) { return smin(smax(t, 0.0f), 1.0f); }  // std::clamp(t, 0, 1)
+TPT_D double clampd(double v) { return v < -1.0 ? -1.0 : (1.0 < v ? 1.0 : v); }
+
+// AnyPerpendicular (SampleHelperFunctions.cpp:51-67)
+TPT_D V3 any_perp(V3 i) {
+    if (i.z == 0.0f) {
+        if (i.y == 0.0f) return v3(0.0f, 1.0f, 0.0f);
+        return normalized(v3(1.0f, -i.x / i.y, 0.0f));
+    }
+    return normalized(v3(0.0f, 1.0f, -1.0f * i.y / i.z));
+}
+// TransformVectorToWorld (SampleHelperFunctions.hpp:46-54)
+TPT_D V3 to_world(V3 a, V3 n) {
+    V3 t = any_perp(n), b = cross(n, t);
+    return v3(a.x * t.x + a.y * b.x + a.z * n.x, a.x * t.y + a.y * b.y + a.z * n.y,
+              a.x * t.z + a.y * b.z + a.z * n.z);
+}
+// Reflect (SampleHelperFunctions.cpp:21-25)
+TPT_D V3 reflect(V3 I, V3 N) {
+    I = -I;
+    return I - mul(N, (float)(2 * dot3(I, N)));
+}
+// Refract (SampleHelperFunctions.cpp:38-49)
+TPT_D V3 refract(V3 I, V3 N, float ior) {
+    I = -I;
+    float cosi = (float)clampd(dot3(I, N));
+    float etai = 1, etat = ior;
+    V3 n = N;
+    if (cosi < 0) cosi = -cosi;
+    else { float t = etai; etai = etat; etat = t; n = -N; }
+    float eta = etai / etat;
+    float k = 1 - eta * eta * (1 - cosi * cosi);
+    return k < 0 ? v3s(0.0f) : normalized(mul(I, eta) + mul(n, eta * cosi - sqrt_f(k)));
+}
+// GetInsideOutsideIOR (SampleHelperFunctions.hpp:57-73)
+TPT_D void inout_ior(V3 N, V3 wi, V3 wo, float mior, float& ior_i, float& ior_o) {
+    float nl = (float)dot3(N, wi), nv = (float)dot3(N, wo);
+    ior_i = nl < 0.0f ? mior : 1.0f;
+    ior_o = nv < 0.0f ? mior : 1.0f;
+}
+// GetHalfDir (SampleHelperFunctions.hpp:79-102)
+TPT_D V3 half_dir(V3 N, V3 wi, V3 wo, float mior) {
+    float nl = (float)dot3(N, wi), nv = (float)dot3(N, wo);
+    if (nl == 0.0f || nv == 0.0f) return v3s(0.0f);
+    if (nl * nv > 0.0f) {
+        V3 h = normalized(wi + wo);
+        return nv < 0.0f ? -h : h;
+    }
+    if (nv < 0.0f) return -normalized(mul(wo, mior) + wi);
+    return -normalized(wo + mul(wi, mior));
+}
+// GetCosineWeightedSample (SampleHelperFunctions.hpp:105-115); cos/sin in double
+TPT_D V3 cosine_sample(V3 N, float& pdf, uint32_t& rs) {
+    float u1 = rng_float(rs);
+    float r = sqrt_f(u1);
+    float theta = 2 * kPi * rng_float(rs);
+    float x = (float)((double)r * cos_d((double)theta)), y = (float)((double)r * sin_d((double)theta));
+    V3 wi = normalized(to_world(v3(x, y, sqrt_f(1.0f - u1)), N));
+    pdf = (float)(dot3(wi, N) / (double)kPi);
+    return wi;
+}
+// GetCosineWeightedPdf (SampleHelperFunctions.hpp:118-120)
+TPT_D float cosine_pdf(V3 N, V3 wi) { return saturate((float)dot3(wi, N)) / kPi; }
+
+// GGX.hpp:8-14
+TPT_D float ggx_vis(float vn, float vh, float r) {
+    if (vh * vn <= 0.0f) return 0.0f;
+    float vh2 = vh * vh;
+    float tan2 = (1.0f - vh2) / vh2;
+    return 2.0f / (1 + sqrt_f(1.0f + r * r * tan2));
+}
+// GGX.hpp:17-30
+TPT_D float ggx_d(float c, float r) {
+    float a2 = r * r;
+    float c2 = c * c;
+    float c4 = c2 * c2;
+    float t2 = (1.0f - c2) / c2;
+    float b = a2 + t2;
+    b = b * b;
+    return a2 / (kPi * c4 * b);
+}
+// GGX.hpp:33-35 (float(|d|) into GGXTerm, product with |d| in double)
+TPT_D float ggx_half_pdf(V3 n, V3 h, float r) {
+    double d = dabs_(dot3(n, h));
+    return (float)((double)ggx_d((float)d, r) * d);
+}
+// GGX.hpp:46-59
+TPT_D V3 ggx_sample_h(V3 N, float r, uint32_t& rs) {
+    float d1 = rng_float(rs), d2 = rng_float(rs);
+    float theta = tpt_atan2f(r * sqrt_f(d1), sqrt_f(1.0f - d1));
+    float phi = 2.0f * kPi * d2;
+    float st = tpt_sinf(theta);
+    V3 local = v3(st * tpt_cosf(phi), st * tpt_sinf(phi), tpt_cosf(theta));
+    return normalized(to_world(local, N));
+}
+
+// Material::fresnel (Material.cpp:221-252)
+TPT_D V3 fresnel(const Mat& m, V3 I, V3 N) {
+    if (m.type == TPT_METAL) {
+        float c = (float)dot3(I, N);
+        float c2 = c * c;
+        V3 two = mul(mul(m.ior_m, 2.0f), c);
+        V3 t0 = m.ior_m * m.ior_m + m.ior_m_k * m.ior_m_k;
+        V3 t1 = mul(t0, c2);
+        V3 Rs = (t0 - two + v3s(c2)) / (t0 + two + v3s(c2));
+        V3 Rp = (t1 - two + v3s(1.0f)) / (t1 + two + v3s(1.0f));
+        return mul(Rp + Rs, 0.5f);
+    }
+    I = -I;
+    float cosi = (float)clampd(dot3(I, N));
+    float etai = 1, etat = m.ior_d;
+    if (cosi > 0) { float t = etai; etai = etat; etat = t; }
+    float sint = etai / etat * sqrt_f(smax(0.f, 1 - cosi * cosi));
+    if (sint >= 1) return v3s(1.0f);
+    float cost = sqrt_f(smax(0.f, 1 - sint * sint));
+    cosi = fabs_(cosi);
+    float Rs = ((etat * cosi) - (etai * cost)) / ((etat * cosi) + (etai * cost));
+    float Rp = ((etai * cosi) - (etat * cost)) / ((etai * cosi) + (etat * cost));
+    return v3s((Rs * Rs + Rp * Rp) / 2);
+}
+
+// Material::evalGivenSample (Material.cpp:11-72)
+TPT_D V3 eval_bsdf(const Mat& m, V3 wo, V3 wi, V3 N, bool cosine) {
+    float nl = (float)dot3(N, wi);
+    float nv = (float)dot3(N, wo);
+    if (nl == 0.0f || nv == 0.0f) return v3s(0.0f);
+    V3 h = half_dir(N, wi, wo, m.ior_d);
+    float nh = (float)dot3(N, h);
+    float lh = (float)dot3(wi, h);
+    float vh = (float)dot3(wo, h);
+    float D = ggx_d(nh, m.rough);
+    float G = ggx_vis(nv, vh, m.rough) * ggx_vis(nl, lh, m.rough);
+    V3 f = fresnel(m, wi, h);
+    if (nl * nv > 0.0f) {
+        V3 spec = v3s(0.0f);
+        if (G != 0.0f) {
+            spec = divs(mul(mul(f, D), G), (float)(4.0 * (double)fabs_(nv)));
+            if (!cosine) spec = divs(spec, fabs_(nl));
+        }
+        V3 diff = v3s(0.0f);
+        if (m.type == TPT_DIELETRIC) {
+            diff = divs(m.kd * (v3s(1.0f) - f), kPi);
+            if (cosine) diff = mul(diff, saturate(nl));
+        }
+        return diff + spec;
+    }
+    if (m.type != TPT_TRANSPARENT) return v3s(0.0f);
+    float ior_i, ior_o;
+    if (nv < 0.0f) { ior_i = 1.0f; ior_o = m.ior_d; }
+    else { ior_i = m.ior_d; ior_o = 1.0f; }
+    float pa = fabs_(vh) * fabs_(lh) / (fabs_(nv));
+    if (!cosine) pa /= fabs_(nl);
+    float pb = ior_o * ior_o * (1.0f - f.x) * G * D;
+    if (pa * pb == 0.0f) return v3s(0.0f);
+    float pc = ior_i * lh + ior_o * vh;
+    pc *= pc;
+    return v3s(pa * pb / pc);
+}
+
+TPT_D float safe_div(float v, float p) { return p == 0.0f ? 0.0f : v / p; }  // SampleHelperFunctions.hpp:24-32
+TPT_D V3 safe_div(V3 v, float p) { return p == 0.0f ? v3s(0.0f) : divs(v, p); }
+
+// Material::pdf (Material.cpp:105-147)
+TPT_D float mat_pdf(const Mat& m, V3 wo, V3 n, V3 wi) {
+    float nv = (float)dot3(n, wo), nl = (float)dot3(n, wi);
+    if (nv == 0.0f || nl == 0.0f) return 0.0f;
+    V3 h = half_dir(n, wi, wo, m.ior_d);
+    V3 f = fresnel(m, wo, h);
+    float pdf_h = ggx_half_pdf(n, h, m.rough);
+    float vh = (float)dot3(wo, h);
+    float avh = fabs_(vh);
+    float lh = (float)dot3(wi, h);
+    float ior_i, ior_o;
+    inout_ior(n, wi, wo, m.ior_d, ior_i, ior_o);
+    if (nv * nl < 0.0f) {
+        float den = ior_i * lh + ior_o * vh;
+        float jac = safe_div(ior_o * ior_o * avh, den * den);
+        if (m.type != TPT_TRANSPARENT) return 0.0f;
+        return pdf_h * (1.0f - f.x) * jac;
+    }
+    if (nv * nl > 0.0f) {
+        float jac = safe_div(1.0f, 4.0f * avh);
+        float diff = cosine_pdf(n, wi);
+        if (m.type == TPT_METAL) return pdf_h * jac;
+        if (m.type == TPT_DIELETRIC) return (diff + pdf_h * jac) * 0.5f;
+        return pdf_h * f.x * jac;
+    }
+    return 0.0f;
+}
+
+// Material::sample (Material.cpp:150-214)
+TPT_D V3 mat_sample(const Mat& m, V3 wo, V3 n, float* pdf, uint32_t& rs) {
+    V3 H = ggx_sample_h(n, m.rough, rs);
+    V3 wis = reflect(wo, H);
+    float pdf_h = ggx_half_pdf(n, H, m.rough);
+    float vn = (float)dot3(wo, n);
+    float vh = (float)dot3(wo, H);
+    float avh = fabs_(vh);
+    float jr = safe_div(1.0f, 4.0f * avh);
+    if (m.type == TPT_METAL) {
+        *pdf = pdf_h * jr;
+        if ((double)vn * dot3(wis, n) < 0.0f) *pdf = 0.0f;
+        return wis;
+    }
+    if (m.type == TPT_DIELETRIC) {
+        if (rng_float(rs) < 0.5f) {
+            float pd = cosine_pdf(n, wis);
+            *pdf = (pdf_h * jr + pd) * 0.5f;
+            if ((double)vn * dot3(wis, n) < 0.0f) *pdf = 0.0f;
+            return wis;
+        }
+        float pd;
+        V3 wid = cosine_sample(n, pd, rs);
+        H = normalized(wid + wo);
+        vh = (float)dot3(wo, H);
+        avh = fabs_(vh);
+        pdf_h = ggx_half_pdf(n, H, m.rough);
+        jr = safe_div(1.0f, 4.0f * avh);
+        *pdf = (pdf_h * jr + pd) * 0.5f;
+        if ((double)vn * dot3(wid, n) < 0.0f) *pdf = 0.0f;
+        return wid;
+    }
+    V3 f = fresnel(m, wo, H);
+    if (rng_float(rs) < f.x) {
+        *pdf = pdf_h * f.x * jr;
+        if ((double)vn * dot3(wis, n) < 0.0f) *pdf = 0.0f;
+        return wis;
+    }
+    V3 wr = refract(wo, H, m.ior_d);
+    float ior_i, ior_o;
+    inout_ior(n, wr, wo, m.ior_d, ior_i, ior_o);
+    float lh = (float)dot3(wr, H);
+    float den = ior_i * lh + ior_o * vh;
+    float jt = safe_div(ior_o * ior_o * avh, den * den);
+    *pdf = pdf_h * (1.0f - f.x) * jt;
+    if ((double)vn * dot3(wr, n) > 0.0f) *pdf = 0.0f;
+    return wr;
+}
+
+// ---------------------------------------------------------- light objects --
+// Object::Sample: BVHAccel::Sample / getSample (BVH.cpp:145-159) + Triangle::Sample
+// (Triangle.hpp:31-36); Sphere::Sample (Sphere.cpp:48-55).
+TPT_D void object_sample(const DScene& s, const DObj& o, V3& pc, V3& pn, int& prim, uint32_t& rs) {
+    if (o.kind == TPT_OBJ_MESH) {
+        float p = sqrt_f(rng_float(rs)) * o.root_area;
+        int ni = o.root;
+        for (;;) {
+            const DNode n = s.nodes[ni];
+            if (n.a < 0) break;
+            const float la = s.node_area[n.a];
+            if (p < la) ni = n.a;
+            else { p = p - la; ni = n.b; }
+        }
+        const int t = -1 - s.nodes[ni].a;
+        const DTri tri = s.tris[t];
+        const DTriX tx = s.trix[t];
+        float x = sqrt_f(rng_float(rs)), y = rng_float(rs);
+        pc = mul(v3(tri.v0[0], tri.v0[1], tri.v0[2]), 1.0f - x) + mul(v3(tx.v1[0], tx.v1[1], tx.v1[2]), x * (1.0f - y)) +
+             mul(v3(tx.v2[0], tx.v2[1], tx.v2[2]), x * y);
+        pn = tri_normal(tri);
+        prim = t;
+    } else {
+        const DSphere sp = s.sph[o.sphere_prim - s.ntri];
+        float theta = (float)(2.0 * (double)kPi * (double)rng_float(rs));
+        float phi = (float)(kPi * rng_float(rs));
+        V3 dir = v3(tpt_cosf(phi), tpt_sinf(phi) * tpt_cosf(theta), tpt_sinf(phi) * tpt_sinf(theta));
+        pc = v3(sp.c[0], sp.c[1], sp.c[2]) + mul(dir, sp.r);
+        pn = dir;
+        prim = o.sphere_prim;
+    }
+}
+
+// Object::GetIntersection for one emitter object, evaluating two culling modes on
+// one ray in a single traversal (the box tests do not depend on culling; the
+// culling test is the first step of each primitive test, Triangle.cpp:81-88).
+struct Hit2 {
+    Hit a, b;
+};
+TPT_D Hit object_hit(const DScene& s, const DObj& o, const Ray& r, int cull, int* stk) {
+    if (o.kind == TPT_OBJ_MESH) return traverse(s, o.root, r, cull, stk);
+    Hit h;
+    h.prim = -1;
+    h.dist = 0.0;
+    double dist;
+    if (sphere_test(s.sph[o.sphere_prim - s.ntri], r, cull, dist)) { h.prim = o.sphere_prim; h.dist = dist; }
+    return h;
+}
+
+// ------------------------------------------------------------------- PT ---
+// PathTrace at HEAD (PathTracer.cpp:44-134): emission of the camera hit + MIS
+// direct lighting from every emitter, then the unconditional `break` (:109).
+// The camera hit is the same for every sample of a pixel (no jitter,
+// SceneRenderingHelper.cpp:16-22) and is hoisted out of the spp loop by the caller.
+struct PTHit {
+    V3 x, n, wo;
+    int mat;
+};
+TPT_D V3 pt_sample(const DScene& s, const PTHit& h, const Mat& m, uint32_t& rs, int* stk) {
+    V3 result = v3s(0.0f);
+    if (s.mats[h.mat].has_em) result = result + m.em;
+    float pdf_b;
+    V3 wib = mat_sample(m, h.wo, h.n, &pdf_b, rs);
+    for (int li = 0; li < s.n_emitters; ++li) {
+        const DObj o = s.objs[s.emitters[li]];
+        // DirectLightSampler::sample (PathTracer.cpp:26-40)
+        V3 pc, pn;
+        int pp;
+        object_sample(s, o, pc, pn, pp, rs);
+        V3 wil = pc - h.x;
+        float d2 = (float)dot3(wil, wil);
+        wil = normalized(wil);
+        float ct = (float)dot3(pn, -wil);
+        float pll = (float)((double)o.pdf * d2 / (double)fabs_(ct));
+        float plb = mat_pdf(m, h.wo, h.n, wil);
+        // DirectLightSampler::pdf (PathTracer.cpp:14-24) on the BSDF direction
+        Ray rb = make_ray(h.x, wib);
+        float pbl = 0.0f;
+        {
+            Hit hb = object_hit(s, o, rb, TPT_NO_CULL, stk);
+            if (hb.prim >= 0) {
+                V3 hx, hn;
+                hit_geometry(s, rb, hb, hx, hn);
+                float ld2 = (float)dot3(hx - h.x, hx - h.x);
+                float c = (float)dot3(hn, -wib);
+                if (c != 0.0f) pbl = (float)((double)o.pdf * ld2 / (double)fabs_(c));
+            }
+        }
+        V3 ev = v3s(0.0f);
+        if (pdf_b + pbl > 0.0f) {
+            Hit hb = object_hit(s, o, rb, TPT_CULL_BACK, stk);
+            if (hb.prim >= 0) {
+                V3 hx, hn;
+                hit_geometry(s, rb, hb, hx, hn);
+                if (!shadow_pts(s, hx, h.x, TPT_CULL_BACK, stk))
+                    ev = ev + divs(eval_bsdf(m, h.wo, wib, h.n, true), 1e-4f + pdf_b + pbl);
+            }
+        }
+        if (pll + plb > 0.0f) {
+            Ray rl = make_ray(h.x, wil);
+            Hit hl = object_hit(s, o, rl, TPT_CULL_BACK, stk);
+            V3 hx = v3s(0.0f), hn;  // default Intersection::coords when missed (Intersection.hpp:14-21)
+            if (hl.prim >= 0) hit_geometry(s, rl, hl, hx, hn);
+            if (!shadow_pts(s, hx, h.x, TPT_CULL_BACK, stk))
+                ev = ev + divs(eval_bsdf(m, h.wo, wil, h.n, true), 1e-4f + pll + plb);
+        }
+        result = result + ev * load_mat(s, o.mat).em;
+    }
+    return result;
+}
+
+// Camera (SceneRenderingHelper.cpp:16-22); scale is host-computed CalculateScale.
+TPT_D V3 pixel_ray(int px, int py, int w, int h, float scale) {
+    float aspect = (float)(w / h);
+    float x = (float)((2 * ((double)px + 0.5) / (double)(float)w - 1) * (double)aspect * (double)scale);
+    float y = (float)((1 - 2 * ((double)py + 0.5) / (double)(float)h) * (double)scale);
+    return normalized(v3(-x, y, 1));
+}
+
+}  // namespace tpt

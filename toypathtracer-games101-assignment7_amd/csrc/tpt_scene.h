@@ -1,0 +1,99 @@
+// tpt_scene.h -- HBM layout of a flattened scene (shared by the host builder and
+// the gfx950 kernels).
+//
+// The reference keeps a two-level BVH of heap objects (Scene::bvh over Object*,
+// one BVHAccel per MeshTriangle: Scene.cpp:11-19, Triangle.cpp:74, BVH.hpp:89-104).
+// Here both levels live in ONE node array:
+//   nodes[0 .. ntop)          scene-level nodes, reference allocation order
+//   nodes[ntop .. nnodes)     each mesh's nodes, reference allocation order
+// A scene-level leaf that holds a mesh is replaced by a copy of that mesh's root
+// node.  The reference tests the leaf box (MeshTriangle::bounding_box) and then the
+// mesh root box (union of the triangle boxes); both are the componentwise min/max
+// of the same vertices, i.e. the same box, so one test is exact.  Traversal order
+// (right child popped first, BVH.cpp:129-132) and closest-hit tie breaking are
+// therefore unchanged (tests/test_gpu_parity.py checks hit ordinals).
+#pragma once
+#include <stdint.h>
+
+namespace tpt {
+
+// 32 B.  a >= 0: interior (a = left, b = right).  a < 0: leaf of primitive -1-a
+// (triangles [0, ntri), spheres [ntri, ntri+nsph)).  a == kEmptyLeaf: empty mesh.
+struct DNode {
+    float bmin[3];
+    int32_t a;
+    float bmax[3];
+    int32_t b;
+};
+static const int32_t kEmptyLeaf = (int32_t)0x80000000;
+
+// 48 B, read as three float4: (v0, n.x) (e1, n.y) (e2, n.z) -- Triangle.hpp:46-50
+struct DTri {
+    float v0[3];
+    float nx;
+    float e1[3];
+    float ny;
+    float e2[3];
+    float nz;
+};
+// 32 B, only touched on light sampling / pdf paths: v1, v2 (Triangle::Sample uses
+// the original vertices, Triangle.hpp:33), area (Triangle::pdf), material.
+struct DTriX {
+    float v1[3];
+    float area;
+    float v2[3];
+    int32_t mat;
+};
+struct DSphere {  // Sphere.hpp:13-15
+    float c[3];
+    float r;
+    float r2;
+    float area;
+    int32_t mat;
+    int32_t pad;
+};
+struct DMat {  // Material.hpp:19-25
+    int32_t type;
+    float em[3];
+    float ior_d;
+    float ior_m[3];
+    float ior_m_k[3];
+    float kd[3];
+    float rough;
+    int32_t has_em;  // Material::hasEmission (Material.hpp:36-39)
+    int32_t pad[2];
+};
+struct DObj {
+    int32_t kind;         // TPT_OBJ_MESH / TPT_OBJ_SPHERE
+    int32_t mat;
+    int32_t root;         // mesh BVH root in nodes[] (-1 if empty)
+    int32_t sphere_prim;  // global primitive id of the sphere
+    float pdf;            // Object::pdf(): MeshTriangle 1/root-area (Triangle.hpp:58-60), Sphere 1/area
+    float root_area;
+    int32_t pad[2];
+};
+
+// Kernel argument: device pointers + constants.
+struct DScene {
+    const DNode* nodes;
+    const float* node_area;  // BVHBuildNode::area (BVH.hpp:94), per node
+    const DTri* tris;
+    const DTriX* trix;
+    const DSphere* sph;
+    const DMat* mats;
+    const DObj* objs;
+    const int32_t* emitters;  // Scene::m_emissionObjects (object ids)
+    int32_t n_emitters;
+    int32_t ntri;
+    int32_t nsph;
+    int32_t nnodes;
+    int32_t nobj;
+    int32_t width;
+    int32_t height;
+    float scale;  // CalculateScale(fov) (SceneRenderingHelper.cpp:12-14), host-computed
+    float eye[3];
+    float bg[3];
+    int32_t max_stack;  // deepest traversal stack any ray can need
+};
+
+}  // namespace tpt

@@ -1,0 +1,323 @@
+// tpt_scene_build.cpp -- host side of tpt_upload_scene: build the reference's
+// two-level BVH on the CPU and flatten it into the HBM layout of tpt_scene.h.
+//
+// Must reproduce the reference's trees node for node, because traversal order
+// decides closest-hit ties and the per-node area sums drive light sampling:
+//   Triangle ctor (e1, e2, normal, area)          Triangle.hpp:18-25
+//   MeshTriangle bounding box / area sum          Triangle.cpp:46-73
+//   BVHAccel::recursiveBuild (median split on the centroid axis of max extent,
+//   std::sort tie order, size-2 special case,
+//   pre-order allocation)                         BVH.cpp:30-99, :161-169
+//   Bounds3 ctor / Union / Centroid / maxExtent   Bounds3.hpp:11-48, :117-131
+//   Sphere area / bounds                          Sphere.hpp:16, Sphere.cpp:43-46
+//   Scene::BuildBVH emitter list                  Scene.cpp:11-19
+// The comparator sorts object indices on the same float keys in the same initial
+// order with the same libstdc++ std::sort, so the permutation is identical.
+// Compiled with -ffp-contract=off (the reference build has no FMA contraction).
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <limits>
+#include <string>
+#include <vector>
+
+#include "../../include/tpt.h"
+#include "tpt_devmath.h"
+#include "tpt_scene.h"
+#include "tpt_scene_build.h"
+
+namespace tpt {
+namespace {
+
+struct Box {
+    V3 mn, mx;
+};
+Box empty_box() {  // Bounds3() -- Bounds3.hpp:14-20
+    Box b;
+    b.mn = v3s(std::numeric_limits<float>::max());
+    b.mx = v3s(std::numeric_limits<float>::lowest());
+    return b;
+}
+V3 vmin(V3 a, V3 b) { return v3(std::min(a.x, b.x), std::min(a.y, b.y), std::min(a.z, b.z)); }
+V3 vmax(V3 a, V3 b) { return v3(std::max(a.x, b.x), std::max(a.y, b.y), std::max(a.z, b.z)); }
+Box join(const Box& a, const Box& b) { return Box{vmin(a.mn, b.mn), vmax(a.mx, b.mx)}; }
+Box join(const Box& a, V3 p) { return Box{vmin(a.mn, p), vmax(a.mx, p)}; }
+Box box2(V3 p, V3 q) {
+    return Box{v3(std::fmin(p.x, q.x), std::fmin(p.y, q.y), std::fmin(p.z, q.z)),
+               v3(std::fmax(p.x, q.x), std::fmax(p.y, q.y), std::fmax(p.z, q.z))};
+}
+V3 centroid(const Box& b) { return mul(b.mn, 0.5f) + mul(b.mx, 0.5f); }
+float axis(V3 v, int a) { return a == 0 ? v.x : (a == 1 ? v.y : v.z); }
+int max_extent(const Box& b) {
+    V3 d = b.mx - b.mn;
+    if (d.x > d.y && d.x > d.z) return 0;
+    if (d.y > d.z) return 1;
+    return 2;
+}
+
+struct BuildNode {
+    Box box;
+    int left = -1, right = -1;
+    int item = -1;
+    float area = 0.0f;
+};
+
+// BVHAccel::recursiveBuild over items with precomputed boxes / areas.
+struct Builder {
+    const std::vector<Box>& box;
+    const std::vector<float>& area;
+    std::vector<BuildNode> nodes;
+    int depth = 0;
+    Builder(const std::vector<Box>& b, const std::vector<float>& a) : box(b), area(a) {}
+
+    int build(std::vector<int> items, int level) {
+        depth = std::max(depth, level);
+        int idx = (int)nodes.size();
+        nodes.emplace_back();
+        if (items.size() == 1) {
+            nodes[idx].box = box[items[0]];
+            nodes[idx].item = items[0];
+            nodes[idx].area = area[items[0]];
+            return idx;
+        }
+        if (items.size() == 2) {
+            int l = build({items[0]}, level + 1);
+            int r = build({items[1]}, level + 1);
+            nodes[idx].left = l;
+            nodes[idx].right = r;
+            nodes[idx].box = join(nodes[l].box, nodes[r].box);
+            nodes[idx].area = nodes[l].area + nodes[r].area;
+            return idx;
+        }
+        Box cb = empty_box();
+        for (int it : items) cb = join(cb, centroid(box[it]));
+        int dim = max_extent(cb);
+        std::sort(items.begin(), items.end(),
+                  [&](int a, int b) { return axis(centroid(box[a]), dim) < axis(centroid(box[b]), dim); });
+        size_t mid = items.size() / 2;
+        int l = build(std::vector<int>(items.begin(), items.begin() + mid), level + 1);
+        int r = build(std::vector<int>(items.begin() + mid, items.end()), level + 1);
+        nodes[idx].left = l;
+        nodes[idx].right = r;
+        nodes[idx].box = join(nodes[l].box, nodes[r].box);
+        nodes[idx].area = nodes[l].area + nodes[r].area;
+        return idx;
+    }
+};
+
+DNode to_dnode(const Box& b, int a, int c) {
+    DNode n;
+    n.bmin[0] = b.mn.x; n.bmin[1] = b.mn.y; n.bmin[2] = b.mn.z;
+    n.bmax[0] = b.mx.x; n.bmax[1] = b.mx.y; n.bmax[2] = b.mx.z;
+    n.a = a;
+    n.b = c;
+    return n;
+}
+
+}  // namespace
+
+int build_host_scene(const tpt_scene_desc* d, HostScene& hs, std::string& err) {
+    hs = HostScene();
+    if (!d || d->width <= 0 || d->height <= 0 || d->num_materials < 0 || d->num_objects < 0) {
+        err = "invalid scene description";
+        return TPT_E_INVALID;
+    }
+    for (int i = 0; i < d->num_materials; ++i) {
+        const tpt_material& m = d->materials[i];
+        if (m.type < 0 || m.type > 2) { err = "invalid material type"; return TPT_E_INVALID; }
+        DMat dm;
+        std::memset(&dm, 0, sizeof(dm));
+        dm.type = m.type;
+        for (int k = 0; k < 3; ++k) {
+            dm.em[k] = m.emission[k];
+            dm.ior_m[k] = m.ior_m[k];
+            dm.ior_m_k[k] = m.ior_m_k[k];
+            dm.kd[k] = m.kd[k];
+        }
+        dm.ior_d = m.ior_d;
+        dm.rough = m.rough;
+        dm.has_em = (m.emission[0] > 0.0f || m.emission[1] > 0.0f || m.emission[2] > 0.0f) ? 1 : 0;
+        hs.mats.push_back(dm);
+    }
+
+    // ---- primitives: all triangles (object order, soup order), then spheres
+    struct MeshRange { int first, count; };
+    std::vector<MeshRange> mesh_tris(d->num_objects, MeshRange{0, 0});
+    std::vector<float> mesh_area(d->num_objects, 0.0f);
+    std::vector<Box> mesh_box(d->num_objects, empty_box());
+    for (int o = 0; o < d->num_objects; ++o) {
+        const tpt_object& ob = d->objects[o];
+        if (ob.material < 0 || ob.material >= d->num_materials) { err = "object material out of range"; return TPT_E_INVALID; }
+        if (ob.kind != TPT_OBJ_MESH) continue;
+        if (ob.first_triangle < 0 || ob.num_triangles < 0 ||
+            3 * ((int64_t)ob.first_triangle + ob.num_triangles) > d->num_vertices) {
+            err = "mesh triangle range out of bounds";
+            return TPT_E_INVALID;
+        }
+        mesh_tris[o].first = (int)hs.tris.size();
+        mesh_tris[o].count = ob.num_triangles;
+        V3 mn = v3s(std::numeric_limits<float>::max()), mx = v3s(-std::numeric_limits<float>::max());
+        for (int t = 0; t < ob.num_triangles; ++t) {
+            V3 v[3];
+            for (int j = 0; j < 3; ++j) {
+                const float* p = d->vertices + 3 * (3 * ((int64_t)ob.first_triangle + t) + j);
+                v[j] = v3(p[0], p[1], p[2]);
+                mn = v3(std::min(mn.x, v[j].x), std::min(mn.y, v[j].y), std::min(mn.z, v[j].z));
+                mx = v3(std::max(mx.x, v[j].x), std::max(mx.y, v[j].y), std::max(mx.z, v[j].z));
+            }
+            V3 e1 = v[1] - v[0], e2 = v[2] - v[0];
+            V3 n = normalized(cross(e1, e2));
+            V3 c = cross(e1, e2);
+            float area = std::sqrt(c.x * c.x + c.y * c.y + c.z * c.z) * 0.5f;
+            DTri dt;
+            dt.v0[0] = v[0].x; dt.v0[1] = v[0].y; dt.v0[2] = v[0].z;
+            dt.e1[0] = e1.x; dt.e1[1] = e1.y; dt.e1[2] = e1.z;
+            dt.e2[0] = e2.x; dt.e2[1] = e2.y; dt.e2[2] = e2.z;
+            dt.nx = n.x; dt.ny = n.y; dt.nz = n.z;
+            DTriX dx;
+            dx.v1[0] = v[1].x; dx.v1[1] = v[1].y; dx.v1[2] = v[1].z;
+            dx.v2[0] = v[2].x; dx.v2[1] = v[2].y; dx.v2[2] = v[2].z;
+            dx.area = area;
+            dx.mat = ob.material;
+            hs.tris.push_back(dt);
+            hs.trix.push_back(dx);
+            hs.tri_object.push_back(o);
+            mesh_area[o] += area;  // MeshTriangle::area, sequential (Triangle.cpp:70-73)
+        }
+        mesh_box[o] = box2(mn, mx);
+    }
+    const int ntri = (int)hs.tris.size();
+    std::vector<int> sphere_prim(d->num_objects, -1);
+    for (int o = 0; o < d->num_objects; ++o) {
+        const tpt_object& ob = d->objects[o];
+        if (ob.kind == TPT_OBJ_MESH) continue;
+        if (ob.kind != TPT_OBJ_SPHERE) { err = "invalid object kind"; return TPT_E_INVALID; }
+        DSphere s;
+        std::memset(&s, 0, sizeof(s));
+        s.c[0] = ob.center[0]; s.c[1] = ob.center[1]; s.c[2] = ob.center[2];
+        s.r = ob.radius;
+        s.r2 = ob.radius * ob.radius;
+        s.area = 4 * kPi * ob.radius * ob.radius;  // Sphere.hpp:16
+        s.mat = ob.material;
+        sphere_prim[o] = ntri + (int)hs.sph.size();
+        hs.sph.push_back(s);
+    }
+
+    // ---- per-mesh BVHs (each mesh's BVHAccel, Triangle.cpp:74)
+    std::vector<Box> tri_box(ntri);
+    std::vector<float> tri_area(ntri);
+    for (int t = 0; t < ntri; ++t) {
+        V3 v0 = v3(hs.tris[t].v0[0], hs.tris[t].v0[1], hs.tris[t].v0[2]);
+        V3 v1 = v3(hs.trix[t].v1[0], hs.trix[t].v1[1], hs.trix[t].v1[2]);
+        V3 v2 = v3(hs.trix[t].v2[0], hs.trix[t].v2[1], hs.trix[t].v2[2]);
+        tri_box[t] = join(box2(v0, v1), v2);  // Triangle::GetBounds, Triangle.hpp:29
+        tri_area[t] = hs.trix[t].area;
+    }
+    struct MeshTree { std::vector<BuildNode> nodes; int depth = 0; };
+    std::vector<MeshTree> mtree(d->num_objects);
+    for (int o = 0; o < d->num_objects; ++o) {
+        if (d->objects[o].kind != TPT_OBJ_MESH || mesh_tris[o].count == 0) continue;
+        Builder b(tri_box, tri_area);
+        std::vector<int> items;
+        for (int t = 0; t < mesh_tris[o].count; ++t) items.push_back(mesh_tris[o].first + t);
+        b.build(items, 1);
+        mtree[o].nodes = std::move(b.nodes);
+        mtree[o].depth = b.depth;
+    }
+
+    // ---- scene-level BVH (Scene::BuildBVH, Scene.cpp:11-13)
+    std::vector<Box> obj_box(d->num_objects);
+    std::vector<float> obj_area(d->num_objects);
+    for (int o = 0; o < d->num_objects; ++o) {
+        if (d->objects[o].kind == TPT_OBJ_MESH) {
+            obj_box[o] = mesh_box[o];
+            obj_area[o] = mesh_area[o];
+        } else {
+            const DSphere& s = hs.sph[sphere_prim[o] - ntri];
+            obj_box[o] = box2(v3(s.c[0] - s.r, s.c[1] - s.r, s.c[2] - s.r), v3(s.c[0] + s.r, s.c[1] + s.r, s.c[2] + s.r));
+            obj_area[o] = s.area;
+        }
+    }
+    Builder top(obj_box, obj_area);
+    if (d->num_objects > 0) {
+        std::vector<int> items;
+        for (int o = 0; o < d->num_objects; ++o) items.push_back(o);
+        top.build(items, 1);
+    }
+
+    // ---- flatten: scene-level nodes first, then each mesh's nodes
+    const int ntop = (int)top.nodes.size();
+    std::vector<int> mesh_base(d->num_objects, -1);
+    int total = ntop;
+    for (int o = 0; o < d->num_objects; ++o)
+        if (!mtree[o].nodes.empty()) { mesh_base[o] = total; total += (int)mtree[o].nodes.size(); }
+    hs.nodes.resize(total);
+    hs.node_area.assign(total, 0.0f);
+    for (int o = 0; o < d->num_objects; ++o) {
+        if (mesh_base[o] < 0) continue;
+        const std::vector<BuildNode>& mn = mtree[o].nodes;
+        for (size_t k = 0; k < mn.size(); ++k) {
+            const BuildNode& n = mn[k];
+            int gi = mesh_base[o] + (int)k;
+            if (n.item >= 0) hs.nodes[gi] = to_dnode(n.box, -1 - n.item, -1);
+            else hs.nodes[gi] = to_dnode(n.box, mesh_base[o] + n.left, mesh_base[o] + n.right);
+            hs.node_area[gi] = n.area;
+        }
+    }
+    int max_depth = 0;
+    // depth of the spliced tree: scene-level depth of the leaf + mesh depth - 1
+    std::vector<int> top_level(ntop, 1);
+    for (int k = 0; k < ntop; ++k) {
+        const BuildNode& n = top.nodes[k];
+        if (n.item < 0) {
+            top_level[n.left] = top_level[k] + 1;
+            top_level[n.right] = top_level[k] + 1;
+            hs.nodes[k] = to_dnode(n.box, n.left, n.right);
+            hs.node_area[k] = n.area;
+            max_depth = std::max(max_depth, top_level[k]);
+            continue;
+        }
+        int o = n.item;
+        if (d->objects[o].kind == TPT_OBJ_MESH) {
+            if (mesh_base[o] < 0) hs.nodes[k] = to_dnode(n.box, kEmptyLeaf, -1);
+            else {
+                DNode root = hs.nodes[mesh_base[o]];
+                hs.nodes[k] = to_dnode(n.box, root.a, root.b);  // identical box, see tpt_scene.h
+            }
+            max_depth = std::max(max_depth, top_level[k] + std::max(mtree[o].depth, 1) - 1);
+        } else {
+            hs.nodes[k] = to_dnode(n.box, -1 - sphere_prim[o], -1);
+            max_depth = std::max(max_depth, top_level[k]);
+        }
+        hs.node_area[k] = n.area;
+    }
+    for (int o = 0; o < d->num_objects; ++o) max_depth = std::max(max_depth, mtree[o].depth);
+    // The reference's push-two stack (BVH.cpp:121-140) holds at most depth+1 entries.
+    hs.max_stack = max_depth + 1;
+
+    // ---- objects and emitters
+    for (int o = 0; o < d->num_objects; ++o) {
+        DObj ob;
+        std::memset(&ob, 0, sizeof(ob));
+        ob.kind = d->objects[o].kind;
+        ob.mat = d->objects[o].material;
+        ob.root = mesh_base[o];
+        ob.sphere_prim = sphere_prim[o];
+        if (ob.kind == TPT_OBJ_MESH) {
+            ob.root_area = mesh_base[o] >= 0 ? hs.node_area[mesh_base[o]] : 0.0f;
+            ob.pdf = 1.0f / ob.root_area;  // MeshTriangle::pdf
+        } else {
+            ob.root_area = hs.sph[sphere_prim[o] - ntri].area;
+            ob.pdf = 1.0f / ob.root_area;  // Sphere::pdf
+        }
+        hs.objs.push_back(ob);
+        if (hs.mats[ob.mat].has_em) hs.emitters.push_back(o);
+    }
+    hs.width = d->width;
+    hs.height = d->height;
+    for (int k = 0; k < 3; ++k) { hs.eye[k] = d->eye[k]; hs.bg[k] = d->background[k]; }
+    hs.fov = d->fov;
+    return TPT_OK;
+}
+
+}  // namespace tpt

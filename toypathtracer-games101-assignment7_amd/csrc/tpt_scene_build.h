@@ -1,0 +1,30 @@
+// tpt_scene_build.h -- host-side flattened scene (input to the HBM upload).
+#pragma once
+#include <string>
+#include <vector>
+
+#include "../../include/tpt.h"
+#include "tpt_scene.h"
+
+namespace tpt {
+
+struct HostScene {
+    std::vector<DNode> nodes;
+    std::vector<float> node_area;
+    std::vector<DTri> tris;
+    std::vector<DTriX> trix;
+    std::vector<int> tri_object;
+    std::vector<DSphere> sph;
+    std::vector<DMat> mats;
+    std::vector<DObj> objs;
+    std::vector<int32_t> emitters;
+    int width = 0, height = 0;
+    float eye[3] = {0, 0, 0};
+    float bg[3] = {0, 0, 0};
+    double fov = 40.0;
+    int max_stack = 1;
+};
+
+int build_host_scene(const tpt_scene_desc* d, HostScene& hs, std::string& err);
+
+}  // namespace tpt
