@@ -1,17 +1,17 @@
 // tpt_capi.hip -- gfx950 kernels of the integration loop + the C ABI (include/tpt.h).
 //
-// Kernel geometry (replay mode): one lane per pixel stream, serial spp loop, which
-// is what the reference's RNG contract requires -- ResetRandom(i+1) once per pixel
-// and ONE XorShift stream through all spp samples (Renderer.cpp:42-52), with a
-// data-dependent number of draws per sample, so sample k of a pixel can only be
-// produced after samples 0..k-1.  784x784 = 614,656 streams =
-// 9,604 wave64s: ~9 waves per SIMD on 256 CUs, enough to fill the chip.
+// Replay contract: ResetRandom(i+1) once per pixel and ONE XorShift stream through
+// all spp samples (Renderer.cpp:42-52).  BDPT's draws per sample depend on the
+// geometry, so a BDPT pixel stream is one lane with a serial spp loop (784x784 =
+// 9,604 wave64s).  PT's draws per sample do not, so PT spreads a pixel's samples
+// over Q lanes (see tpt_pt_kernel).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -24,25 +24,91 @@
 using namespace tpt;
 
 // ------------------------------------------------------------------ kernels --
-// PT: Renderer.cpp:38-52 for TPT_MODE_PT.  Pixels are {begin + k*stride} or
-// list[k]; rgb row = pixel index (full frame) or k (list).
-__global__ __launch_bounds__(kBlock) void tpt_pt_kernel(DScene s, int spp, int64_t begin, int64_t stride,
-                                                        int64_t count, const int64_t* __restrict__ list,
-                                                        float* __restrict__ out) {
-    __shared__ int stack[kStackCap * kBlock];
-    int* stk = stack + threadIdx.x;
-    const int64_t k = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (k >= count) return;
-    const int64_t i = list ? list[k] : begin + k * stride;
+extern __shared__ __align__(16) unsigned char tpt_smem[];
+
+// Per-wave packet stacks (4 waves per workgroup).
+#define TPT_PACKET_DECL                                                   \
+    __shared__ int pk_node[kBlock / 64][kStackCap];                       \
+    __shared__ unsigned long long pk_mask[kBlock / 64][kStackCap];        \
+    Packet pk;                                                            \
+    pk.node = pk_node[threadIdx.x / 64];                                  \
+    pk.mask = pk_mask[threadIdx.x / 64];
+
+// Workgroup prologue: LDS = [traversal stack: max_stack x kBlock ints][nodes][tris].
+// With kLds the scene's node and triangle arrays are copied into LDS (16 B per lane
+// per step) and the kernel's DScene is pointed at them, so every traversal fetch is
+// a ds_read instead of a dependent L1/L2 load.
+template <bool kLds>
+TPT_D int* stage_scene(DScene& s) {
+    int* stk = reinterpret_cast<int*>(tpt_smem) + threadIdx.x;
+    if (kLds) {
+        unsigned char* base = tpt_smem + (size_t)s.max_stack * kBlock * sizeof(int);
+        const int nb = s.nnodes * (int)sizeof(DNode), tb = s.ntri * (int)sizeof(DTri);
+        const uint4* gn = reinterpret_cast<const uint4*>(s.nodes);
+        const uint4* gt = reinterpret_cast<const uint4*>(s.tris);
+        uint4* ln = reinterpret_cast<uint4*>(base);
+        uint4* lt = reinterpret_cast<uint4*>(base + nb);
+        for (int i = threadIdx.x; i < nb / 16; i += kBlock) ln[i] = gn[i];
+        for (int i = threadIdx.x; i < tb / 16; i += kBlock) lt[i] = gt[i];
+        __syncthreads();
+        s.nodes = reinterpret_cast<const DNode*>(base);
+        s.tris = reinterpret_cast<const DTri*>(base + nb);
+    }
+    return stk;
+}
+
+#ifndef TPT_PT_MINWAVES
+#define TPT_PT_MINWAVES 3  // waves per SIMD the PT kernel's register budget must allow (3 measured best)
+#endif
+
+// PT (Renderer.cpp:38-52 with PathTrace), replay-exact, Q lanes per pixel.
+//
+// PathTrace at HEAD draws, per sample: 2 (GGX half vector) + 1 coin (Dieletric,
+// Transparent) + 2 more iff a Dieletric coin >= 0.5 (cosine sample) + 3 per mesh
+// emitter / 2 per sphere emitter (light sampling) -- a count that depends only on
+// the first-hit material and the coin value, never on geometry (Material.cpp:150-214,
+// PathTracer.cpp:76-86, BVH.cpp:156, Triangle.hpp:32).  So the XorShift state at the
+// start of sample k of a pixel is reached by stepping the stream without tracing.
+// Lane q of the Q lanes that share a pixel takes samples q, q+Q, q+2Q, ... and skips
+// the Q-1 samples in between (~45 VALU ops per skipped sample vs ~4,800 per traced
+// one); after every round the Q radiances are folded into the pixel in sample order,
+// `fb[i] += (1.0f/spp) * L` exactly as Renderer.cpp:49-51.  Q = 1 is one lane per
+// pixel stream; Q > 1 multiplies the parallelism (multi-GPU shards, small frames).
+// The first hit is identical for every sample (no jitter) and is hoisted.
+TPT_D uint32_t skip_samples(uint32_t st, int type, int light_draws, int n) {
+    for (int j = 0; j < n; ++j) {
+        xorshift32(st);
+        xorshift32(st);
+        if (type == TPT_DIELETRIC) {
+            if (rng_float(st) >= 0.5f) { xorshift32(st); xorshift32(st); }
+        } else if (type == TPT_TRANSPARENT) {
+            xorshift32(st);
+        }
+        for (int d = 0; d < light_draws; ++d) xorshift32(st);
+    }
+    return st;
+}
+
+template <bool kLds>
+__global__ __launch_bounds__(kBlock, TPT_PT_MINWAVES) void tpt_pt_kernel(DScene s, int spp, int64_t begin,
+                                                                        int64_t stride, int64_t count,
+                                                                        const int64_t* __restrict__ list,
+                                                                        float* __restrict__ out, int Q) {
+    int* stk = stage_scene<kLds>(s);
+    TPT_PACKET_DECL
+    const int64_t gl = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const int64_t k = gl / Q;      // pixel ordinal in the shard / list
+    const int q = (int)(gl % Q);   // this lane's sample phase
+    const bool on = k < count;
+    const int64_t i = on ? (list ? list[k] : begin + k * stride) : 0;
     const int64_t row = list ? k : i;
     const int px = (int)(i % s.width), py = (int)(i / s.width);
     const V3 dir = pixel_ray(px, py, s.width, s.height, s.scale);
-    const V3 eye = v3(s.eye[0], s.eye[1], s.eye[2]);
-    const Ray r = make_ray(eye, dir);
+    const Ray r = make_ray(v3(s.eye[0], s.eye[1], s.eye[2]), dir);
     PTV v = scene_intersect(s, r, TPT_CULL_BACK, stk);
+    const bool hit = on && v.type != T_BG;
     V3 acc = v3s(0.0f);
-    if (v.type != T_BG) {
-        uint32_t rs = (uint32_t)((int)i + 1);
+    if (hit) {
         PTHit h;
         h.x = v.x;
         h.n = v.N;
@@ -50,22 +116,43 @@ __global__ __launch_bounds__(kBlock) void tpt_pt_kernel(DScene s, int spp, int64
         h.mat = prim_mat(s, v.prim);
         const Mat m = load_mat(s, h.mat);
         const float inv = 1.0f / spp;
-        for (int j = 0; j < spp; ++j) acc = acc + mul(pt_sample(s, h, m, rs, stk), inv);
+        uint32_t rs = (uint32_t)((int)i + 1);  // ResetRandom(i + 1), Renderer.cpp:42
+        rs = skip_samples(rs, m.type, s.light_draws, q);
+        const int base = lane_id() - q;       // first lane of this pixel (Q divides 64)
+        for (int j0 = 0; j0 < spp; j0 += Q) {
+            V3 L = v3s(0.0f);
+            if (j0 + q < spp) {
+                L = mul(pt_sample(s, h, m, rs, stk, pk), inv);
+                if (Q > 1) rs = skip_samples(rs, m.type, s.light_draws, Q - 1);
+            }
+            if (Q == 1) {
+                acc = acc + L;
+            } else {
+                const int n = spp - j0 < Q ? spp - j0 : Q;
+                for (int jj = 0; jj < n; ++jj) {
+                    acc.x = acc.x + __shfl(L.x, base + jj);
+                    acc.y = acc.y + __shfl(L.y, base + jj);
+                    acc.z = acc.z + __shfl(L.z, base + jj);
+                }
+            }
+        }
     }
-    out[3 * row + 0] = acc.x;
-    out[3 * row + 1] = acc.y;
-    out[3 * row + 2] = acc.z;
+    if (on && q == 0) {
+        out[3 * row + 0] = acc.x;
+        out[3 * row + 1] = acc.y;
+        out[3 * row + 2] = acc.z;
+    }
 }
 
 // BDPT: Renderer.cpp:38-52 + :58-60 for TPT_MODE_BDPT.  t=1 strategies splat into
 // `splat` with fp32 atomics (the reference sums per-thread buffers instead,
 // Renderer.cpp:98-114: same values, different summation order).
+template <bool kLds>
 __global__ __launch_bounds__(kBlock) void tpt_bdpt_kernel(DScene s, int spp, int64_t begin, int64_t stride,
                                                           int64_t count, const int64_t* __restrict__ list,
                                                           float* __restrict__ out, float* __restrict__ splat,
                                                           unsigned long long* __restrict__ bounces) {
-    __shared__ int stack[kStackCap * kBlock];
-    int* stk = stack + threadIdx.x;
+    int* stk = stage_scene<kLds>(s);
     const int64_t k = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (k >= count) return;
     const int64_t i = list ? list[k] : begin + k * stride;
@@ -87,8 +174,7 @@ __global__ void tpt_scale_kernel(float* __restrict__ buf, int64_t n, float spp) 
 // Closest-hit queries (Scene::Intersect) for tpt_intersect.
 __global__ __launch_bounds__(kBlock) void tpt_intersect_kernel(DScene s, const float* __restrict__ rays, int64_t n,
                                                                int cull, float* __restrict__ out) {
-    __shared__ int stack[kStackCap * kBlock];
-    int* stk = stack + threadIdx.x;
+    int* stk = stage_scene<false>(s);
     const int64_t k = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (k >= n) return;
     const float* q = rays + 6 * k;
@@ -119,6 +205,7 @@ struct tpt_ctx {
     float* rows = nullptr;
     int64_t rows_cap = 0;
     unsigned long long* counters = nullptr;
+    int pt_lanes = 2;  // Q: lanes per pixel of the PT kernel (1, 2, 4, 8)
 };
 
 namespace {
@@ -171,14 +258,26 @@ int launch(tpt_ctx* c, int mode, int spp, int64_t begin, int64_t stride, int64_t
            float* drows, float* dsplat, tpt_stats* st) {
     if (count <= 0) return TPT_OK;
     const int64_t blocks = (count + kBlock - 1) / kBlock;
-    HIP_TRY(c, hipMemsetAsync(c->counters, 0, sizeof(unsigned long long) * 4, c->stream));
+    HIP_TRY(c, hipMemsetAsync(c->counters, 0, sizeof(unsigned long long) * 16, c->stream));
     HIP_TRY(c, hipEventRecord(c->ev0, c->stream));
+    const bool lds = c->ds.lds_bytes > 0;
+    const size_t shmem = (size_t)c->ds.max_stack * kBlock * sizeof(int) + (size_t)c->ds.lds_bytes;
     if (mode == TPT_MODE_PT) {
-        hipLaunchKernelGGL(tpt_pt_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, c->stream, c->ds, spp, begin,
-                           stride, count, dlist, drows);
+        const int Q = c->pt_lanes;
+        const int64_t qblocks = (count * Q + kBlock - 1) / kBlock;
+        if (lds)
+            hipLaunchKernelGGL(tpt_pt_kernel<true>, dim3((unsigned)qblocks), dim3(kBlock), shmem, c->stream, c->ds,
+                               spp, begin, stride, count, dlist, drows, Q);
+        else
+            hipLaunchKernelGGL(tpt_pt_kernel<false>, dim3((unsigned)qblocks), dim3(kBlock), shmem, c->stream, c->ds,
+                               spp, begin, stride, count, dlist, drows, Q);
     } else {
-        hipLaunchKernelGGL(tpt_bdpt_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, c->stream, c->ds, spp, begin,
-                           stride, count, dlist, drows, dsplat, c->counters);
+        if (lds)
+            hipLaunchKernelGGL(tpt_bdpt_kernel<true>, dim3((unsigned)blocks), dim3(kBlock), shmem, c->stream, c->ds,
+                               spp, begin, stride, count, dlist, drows, dsplat, c->counters);
+        else
+            hipLaunchKernelGGL(tpt_bdpt_kernel<false>, dim3((unsigned)blocks), dim3(kBlock), shmem, c->stream, c->ds,
+                               spp, begin, stride, count, dlist, drows, dsplat, c->counters);
     }
     HIP_TRY(c, hipGetLastError());
     HIP_TRY(c, hipEventRecord(c->ev1, c->stream));
@@ -198,6 +297,12 @@ int launch(tpt_ctx* c, int mode, int spp, int64_t begin, int64_t stride, int64_t
         unsigned long long nb = 0;
         HIP_TRY(c, hipMemcpy(&nb, c->counters, sizeof(nb), hipMemcpyDeviceToHost));
         st->bounces = (int64_t)nb;
+    }
+    if (c->ds.dbg & 2) {  // profiling counters (TPT_DEBUG_FLAGS & 2)
+        unsigned long long d[8];
+        HIP_TRY(c, hipMemcpy(d, c->counters + 8, sizeof(d), hipMemcpyDeviceToHost));
+        std::fprintf(stderr, "[tpt dbg] shadow wave-calls %llu iters/call %.2f leaf-iters/call %.2f lanes/call %.1f\n",
+                     d[0], (double)d[1] / d[0], (double)d[3] / d[0], (double)d[5] / d[0]);
     }
     return TPT_OK;
 }
@@ -231,7 +336,7 @@ int tpt_create(int device, tpt_ctx** out) {
     }
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
-        hipMalloc(&c->counters, sizeof(unsigned long long) * 4) != hipSuccess) {
+        hipMalloc(&c->counters, sizeof(unsigned long long) * 16) != hipSuccess) {
         delete c;
         return TPT_E_DEVICE;
     }
@@ -282,6 +387,9 @@ int tpt_upload_scene(tpt_ctx* c, const tpt_scene_desc* d) {
     ds.objs = (const DObj*)(b + o_objs);
     ds.emitters = (const int32_t*)(b + o_em);
     ds.n_emitters = (int)hs.emitters.size();
+    // BVHAccel::Sample (1 draw) + Triangle::Sample (2) per mesh emitter, Sphere::Sample (2)
+    ds.light_draws = 0;
+    for (int e : hs.emitters) ds.light_draws += hs.objs[e].kind == TPT_OBJ_MESH ? 3 : 2;
     ds.ntri = (int)hs.tris.size();
     ds.nsph = (int)hs.sph.size();
     ds.nnodes = (int)hs.nodes.size();
@@ -291,6 +399,19 @@ int tpt_upload_scene(tpt_ctx* c, const tpt_scene_desc* d) {
     ds.scale = camera_scale(hs.fov);
     for (int k = 0; k < 3; ++k) { ds.eye[k] = hs.eye[k]; ds.bg[k] = hs.bg[k]; }
     ds.max_stack = hs.max_stack;
+    // Stage nodes + triangles in LDS when they fit next to the stack (<= 96 KB per
+    // workgroup keeps >= 1 workgroup per CU; the Cornell presets need ~4 KB).
+    {
+        const size_t sb = hs.nodes.size() * sizeof(DNode) + hs.tris.size() * sizeof(DTri);
+        const char* no = std::getenv("TPT_NO_LDS");
+        ds.lds_bytes = (sb <= 64 * 1024 && !(no && no[0] == '1')) ? (int)sb : 0;
+        const char* dbg = std::getenv("TPT_DEBUG_FLAGS");
+        ds.dbg = dbg ? std::atoi(dbg) : 0;
+        ds.dbgc = c->counters + 8;
+        const char* q = std::getenv("TPT_PT_LANES");
+        c->pt_lanes = q ? std::atoi(q) : 2;  // Q = 2 measured best on one MI355X (Standard, 1024 spp)
+        if (c->pt_lanes != 1 && c->pt_lanes != 2 && c->pt_lanes != 4 && c->pt_lanes != 8) c->pt_lanes = 1;
+    }
     c->ds = ds;
     c->hs = std::move(hs);
     c->has_scene = true;
@@ -372,8 +493,8 @@ int tpt_intersect(tpt_ctx* c, const float* rays, int64_t n, int32_t cull, float*
     int rc = TPT_OK;
     if (hipMemcpy(dr, rays, n * 6 * sizeof(float), hipMemcpyHostToDevice) != hipSuccess) rc = TPT_E_DEVICE;
     if (!rc) {
-        hipLaunchKernelGGL(tpt_intersect_kernel, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0,
-                           c->stream, c->ds, dr, n, cull, dout);
+        hipLaunchKernelGGL(tpt_intersect_kernel, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock),
+                           (size_t)c->ds.max_stack * kBlock * sizeof(int), c->stream, c->ds, dr, n, cull, dout);
         if (hipGetLastError() != hipSuccess || hipStreamSynchronize(c->stream) != hipSuccess ||
             hipMemcpy(out, dout, n * 8 * sizeof(float), hipMemcpyDeviceToHost) != hipSuccess)
             rc = TPT_E_DEVICE;

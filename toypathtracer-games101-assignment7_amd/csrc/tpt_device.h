@@ -21,17 +21,21 @@ namespace tpt {
 #define TPT_D __device__ __forceinline__
 
 constexpr int kBlock = 256;     // threads per workgroup (4 waves)
-constexpr int kStackCap = 32;   // LDS stack entries per lane (upload rejects deeper trees)
+constexpr int kStackCap = 40;   // max LDS stack entries per lane (upload rejects deeper trees)
 
 // ------------------------------------------------------------------ rays --
 struct Ray {
     V3 o, d, inv;
 };
-TPT_D Ray make_ray(V3 o, V3 d) {  // Ray.hpp:12-15
+// Ray.hpp:12-15 computes float(1.0 / (double)d).  A single correctly rounded
+// operation on floats carried out in double and rounded to float equals the
+// correctly rounded float operation (double rounding is innocuous since
+// 53 >= 2*24 + 2), so the exact f32 divide is used.
+TPT_D Ray make_ray(V3 o, V3 d) {
     Ray r;
     r.o = o;
     r.d = d;
-    r.inv = v3((float)(1. / (double)d.x), (float)(1. / (double)d.y), (float)(1. / (double)d.z));
+    r.inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
     return r;
 }
 
@@ -197,16 +201,159 @@ TPT_D PTV scene_intersect(const DScene& s, const Ray& r, int cull, int* stk) {
     }
     return v;
 }
-// Scene::ShadowCheck(Vector3f, Vector3f, FaceCulling) (Scene.cpp:37-48)
+// Scene::ShadowCheck(Vector3f, Vector3f, FaceCulling) (Scene.cpp:37-48):
+// shadowed iff the CLOSEST hit of the ray lc -> x has |hit - lc|^2 < |x - lc|^2 - 1.
+// The hit point is lc + float(t)*d rounded per component and its squared distance
+// is summed in double: every step is monotone, so d2(t) is non-decreasing in t and
+// "closest hit's d2 < thr"  <=>  "some reachable hit's d2 < thr".  Hence an any-hit
+// traversal with early exit is exact.  A qualifying hit lies on the segment
+// [0, T], T ~ sqrt(thr); nodes whose box misses that segment's (padded) AABB cannot
+// contain one and are skipped.  Box tests themselves are the reference's, so the
+// set of reachable primitives is unchanged.
+TPT_D bool box_overlap(const DNode& n, V3 lo, V3 hi) {
+    return !(n.bmin[0] > hi.x || n.bmax[0] < lo.x || n.bmin[1] > hi.y || n.bmax[1] < lo.y || n.bmin[2] > hi.z ||
+             n.bmax[2] < lo.z);
+}
 TPT_D bool shadow_pts(const DScene& s, V3 lc, V3 x, int cull, int* stk) {
-    double ld2 = dot3(lc - x, lc - x);
-    Ray r = make_ray(lc, normalized(x - lc));
-    Hit h = traverse(s, 0, r, cull, stk);
-    if (h.prim < 0) return false;
-    V3 hx, hn;
-    hit_geometry(s, r, h, hx, hn);
-    double sd2 = dot3(hx - lc, hx - lc);
-    return sd2 < ld2 - 1.0f;
+    if (s.dbg & 1) return false;  // profiling ablation only
+    const double ld2 = dot3(lc - x, lc - x);
+    const double thr = ld2 - 1.0f;
+    if (!(thr > 0.0)) return false;  // d2 >= 0 can never be < thr
+    const Ray r = make_ray(lc, normalized(x - lc));
+    const float T = (float)(sqrt_d(thr) * 1.0001 + 0.01);
+    const V3 e = v3(r.o.x + T * r.d.x, r.o.y + T * r.d.y, r.o.z + T * r.d.z);
+    const float pad = 0.01f + 1e-4f * T;
+    const V3 lo = v3(fminf(r.o.x, e.x) - pad, fminf(r.o.y, e.y) - pad, fminf(r.o.z, e.z) - pad);
+    const V3 hi = v3(fmaxf(r.o.x, e.x) + pad, fmaxf(r.o.y, e.y) + pad, fmaxf(r.o.z, e.z) + pad);
+    int sp = 1;
+    stk[0] = 0;
+    while (sp > 0) {
+        --sp;
+        const DNode n = s.nodes[stk[sp * kBlock]];
+        if (!box_overlap(n, lo, hi) || !box_hit(n, r)) continue;
+        if (n.a >= 0) {
+            stk[sp * kBlock] = n.a;
+            stk[(sp + 1) * kBlock] = n.b;
+            sp += 2;
+            continue;
+        }
+        if (n.a == kEmptyLeaf) continue;
+        const int prim = -1 - n.a;
+        double dist;
+        bool h;
+        if (prim < s.ntri) h = tri_test(s.tris[prim], r, cull, dist);
+        else h = sphere_test(s.sph[prim - s.ntri], r, cull, dist);
+        if (h) {
+            const V3 hx = r.o + mul(r.d, (float)dist);
+            if (dot3(hx - lc, hx - lc) < thr) return true;
+        }
+    }
+    return false;
+}
+
+// ------------------------------------------------------- wave packets --
+// Wave-packet traversal: the 64 lanes of a wave walk ONE depth-first node sequence
+// (reference order: right child popped first) held in a wave-uniform LDS stack of
+// {node, lane mask}.  A lane's mask bit is set on a node iff every ancestor box
+// passed that lane's ray test (BVH.cpp:121-137 pushes children of a node whose
+// box passed), so each lane evaluates exactly the boxes and primitives the
+// reference evaluates for its ray, in the same relative order.  Node fetches are
+// wave-uniform (LDS broadcast / scalar loads), the per-iteration cost is one box
+// test, and a primitive test runs only on iterations that are leaves, with the
+// lanes that reached that leaf -- instead of every lane paying for the leaf test of
+// whichever lane happens to be at a leaf.
+struct Packet {
+    int* node;                  // [kStackCap] wave-uniform stack, LDS
+    unsigned long long* mask;   // [kStackCap]
+};
+TPT_D int lane_id() { return __lane_id(); }
+TPT_D int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+TPT_D unsigned long long uni64(unsigned long long v) {
+    const unsigned lo = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)v);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(v >> 32));
+    return ((unsigned long long)hi << 32) | lo;
+}
+
+// Packet form of shadow_pts (same decision per lane, see the exactness note there).
+// Children are box-tested together at their parent (both tests are independent,
+// so they overlap in the pipeline) and the walk descends without a stack round
+// trip; a node's mask holds the lanes whose ray passed that node's own box.
+TPT_D bool shadow_pts_packet(const DScene& s, V3 lc, V3 x, int cull, Packet pk) {
+    const double ld2 = dot3(lc - x, lc - x);
+    const double thr = ld2 - 1.0f;
+    bool done = !(thr > 0.0);  // done lanes have their answer in `shadowed`
+    bool shadowed = false;
+    if (s.dbg & 1) done = true;  // profiling ablation only
+    const Ray r = make_ray(lc, normalized(x - lc));
+    const float T = (float)(sqrt_d(thr > 0.0 ? thr : 0.0) * 1.0001 + 0.01);
+    const V3 e = v3(r.o.x + T * r.d.x, r.o.y + T * r.d.y, r.o.z + T * r.d.z);
+    const float pad = 0.01f + 1e-4f * T;
+    const V3 lo = v3(fminf(r.o.x, e.x) - pad, fminf(r.o.y, e.y) - pad, fminf(r.o.z, e.z) - pad);
+    const V3 hi = v3(fmaxf(r.o.x, e.x) + pad, fmaxf(r.o.y, e.y) + pad, fmaxf(r.o.z, e.z) + pad);
+    unsigned long long live = uni64(__ballot(!done));
+    if (live == 0) return shadowed;
+    unsigned long long it_all = 0, it_leaf = 0;
+    int sp = 0;
+    int cur = 0;
+    unsigned long long m;
+    {
+        const DNode n = s.nodes[0];
+        m = uni64(__ballot(!done && box_overlap(n, lo, hi) && box_hit(n, r)));
+    }
+    for (;;) {
+        ++it_all;
+        if (m != 0) {
+            const DNode n = s.nodes[cur];
+            if (n.a >= 0) {
+                const DNode L = s.nodes[n.a];
+                const DNode R = s.nodes[n.b];
+                const bool mine = (m >> lane_id()) & 1ull;
+                const bool hl = mine && box_overlap(L, lo, hi) && box_hit(L, r);
+                const bool hr = mine && box_overlap(R, lo, hi) && box_hit(R, r);
+                const unsigned long long ml = uni64(__ballot(hl)), mr = uni64(__ballot(hr));
+                if (mr != 0) {  // right subtree first (BVH.cpp:129-132), left deferred
+                    if (ml != 0) {
+                        if (lane_id() == __builtin_ctzll(ml)) { pk.node[sp] = n.a; pk.mask[sp] = ml; }
+                        ++sp;
+                    }
+                    cur = n.b;
+                    m = mr;
+                    continue;
+                }
+                if (ml != 0) { cur = n.a; m = ml; continue; }
+            } else if (n.a != kEmptyLeaf) {
+                ++it_leaf;
+                if ((m >> lane_id()) & 1ull) {
+                    const int prim = -1 - n.a;
+                    double dist;
+                    bool h;
+                    if (prim < s.ntri) h = tri_test(s.tris[prim], r, cull, dist);
+                    else h = sphere_test(s.sph[prim - s.ntri], r, cull, dist);
+                    if (h) {
+                        const V3 hx = r.o + mul(r.d, (float)dist);
+                        if (dot3(hx - lc, hx - lc) < thr) { shadowed = true; done = true; }
+                    }
+                }
+                live = uni64(__ballot(!done)) & live;
+                if (live == 0) break;
+            }
+        }
+        if (sp == 0) break;
+        --sp;
+        cur = uni(pk.node[sp]);
+        m = uni64(pk.mask[sp]) & live;
+    }
+    if (s.dbg & 2) {
+        const unsigned long long act = __ballot(1);
+        if (lane_id() == __builtin_ctzll(act)) {
+            atomicAdd(s.dbgc + 0, 1ull);
+            atomicAdd(s.dbgc + 1, it_all);
+            atomicAdd(s.dbgc + 2, it_all);
+            atomicAdd(s.dbgc + 3, it_leaf);
+            atomicAdd(s.dbgc + 5, (unsigned long long)__popcll(act));
+        }
+    }
+    return shadowed;
 }
 
 // ------------------------------------------------------------ materials --
@@ -506,6 +653,41 @@ TPT_D void object_sample(const DScene& s, const DObj& o, V3& pc, V3& pn, int& pr
 struct Hit2 {
     Hit a, b;
 };
+// NoCull and CullBack closest hits of one ray against one emitter object, one
+// traversal (same node order, same strict `>` tie rule for each result).
+TPT_D void object_hit_nocull_back(const DScene& s, const DObj& o, const Ray& r, Hit& hn, Hit& hb, int* stk) {
+    hn.prim = hb.prim = -1;
+    hn.dist = hb.dist = 0.0;
+    if (o.kind != TPT_OBJ_MESH) {
+        double d;
+        const DSphere sp = s.sph[o.sphere_prim - s.ntri];
+        if (sphere_test(sp, r, TPT_NO_CULL, d)) { hn.prim = o.sphere_prim; hn.dist = d; }
+        if (sphere_test(sp, r, TPT_CULL_BACK, d)) { hb.prim = o.sphere_prim; hb.dist = d; }
+        return;
+    }
+    if (o.root < 0) return;
+    int sp = 1;
+    stk[0] = o.root;
+    while (sp > 0) {
+        --sp;
+        const DNode n = s.nodes[stk[sp * kBlock]];
+        if (!box_hit(n, r)) continue;
+        if (n.a >= 0) {
+            stk[sp * kBlock] = n.a;
+            stk[(sp + 1) * kBlock] = n.b;
+            sp += 2;
+            continue;
+        }
+        if (n.a == kEmptyLeaf) continue;
+        const int prim = -1 - n.a;
+        const DTri t = s.tris[prim];
+        double d;
+        if (!tri_test(t, r, TPT_NO_CULL, d)) continue;  // culling is the test's first step
+        if (hn.prim < 0 || hn.dist > d) { hn.prim = prim; hn.dist = d; }
+        if (!(dot3(r.d, tri_normal(t)) > 0) && (hb.prim < 0 || hb.dist > d)) { hb.prim = prim; hb.dist = d; }
+    }
+}
+
 TPT_D Hit object_hit(const DScene& s, const DObj& o, const Ray& r, int cull, int* stk) {
     if (o.kind == TPT_OBJ_MESH) return traverse(s, o.root, r, cull, stk);
     Hit h;
@@ -525,7 +707,7 @@ struct PTHit {
     V3 x, n, wo;
     int mat;
 };
-TPT_D V3 pt_sample(const DScene& s, const PTHit& h, const Mat& m, uint32_t& rs, int* stk) {
+TPT_D V3 pt_sample(const DScene& s, const PTHit& h, const Mat& m, uint32_t& rs, int* stk, Packet pk) {
     V3 result = v3s(0.0f);
     if (s.mats[h.mat].has_em) result = result + m.em;
     float pdf_b;
@@ -544,24 +726,22 @@ TPT_D V3 pt_sample(const DScene& s, const PTHit& h, const Mat& m, uint32_t& rs, 
         float plb = mat_pdf(m, h.wo, h.n, wil);
         // DirectLightSampler::pdf (PathTracer.cpp:14-24) on the BSDF direction
         Ray rb = make_ray(h.x, wib);
+        Hit hnc, hb;
+        object_hit_nocull_back(s, o, rb, hnc, hb, stk);
         float pbl = 0.0f;
-        {
-            Hit hb = object_hit(s, o, rb, TPT_NO_CULL, stk);
-            if (hb.prim >= 0) {
-                V3 hx, hn;
-                hit_geometry(s, rb, hb, hx, hn);
-                float ld2 = (float)dot3(hx - h.x, hx - h.x);
-                float c = (float)dot3(hn, -wib);
-                if (c != 0.0f) pbl = (float)((double)o.pdf * ld2 / (double)fabs_(c));
-            }
+        if (hnc.prim >= 0) {
+            V3 hx, hn;
+            hit_geometry(s, rb, hnc, hx, hn);
+            float ld2 = (float)dot3(hx - h.x, hx - h.x);
+            float c = (float)dot3(hn, -wib);
+            if (c != 0.0f) pbl = (float)((double)o.pdf * ld2 / (double)fabs_(c));
         }
         V3 ev = v3s(0.0f);
         if (pdf_b + pbl > 0.0f) {
-            Hit hb = object_hit(s, o, rb, TPT_CULL_BACK, stk);
             if (hb.prim >= 0) {
                 V3 hx, hn;
                 hit_geometry(s, rb, hb, hx, hn);
-                if (!shadow_pts(s, hx, h.x, TPT_CULL_BACK, stk))
+                if (!shadow_pts_packet(s, hx, h.x, TPT_CULL_BACK, pk))
                     ev = ev + divs(eval_bsdf(m, h.wo, wib, h.n, true), 1e-4f + pdf_b + pbl);
             }
         }
@@ -570,7 +750,7 @@ TPT_D V3 pt_sample(const DScene& s, const PTHit& h, const Mat& m, uint32_t& rs, 
             Hit hl = object_hit(s, o, rl, TPT_CULL_BACK, stk);
             V3 hx = v3s(0.0f), hn;  // default Intersection::coords when missed (Intersection.hpp:14-21)
             if (hl.prim >= 0) hit_geometry(s, rl, hl, hx, hn);
-            if (!shadow_pts(s, hx, h.x, TPT_CULL_BACK, stk))
+            if (!shadow_pts_packet(s, hx, h.x, TPT_CULL_BACK, pk))
                 ev = ev + divs(eval_bsdf(m, h.wo, wil, h.n, true), 1e-4f + pll + plb);
         }
         result = result + ev * load_mat(s, o.mat).em;

@@ -84,6 +84,7 @@ struct DScene {
     const DObj* objs;
     const int32_t* emitters;  // Scene::m_emissionObjects (object ids)
     int32_t n_emitters;
+    int32_t light_draws;  // XorShift draws of one DirectLightSampler::sample pass over all emitters
     int32_t ntri;
     int32_t nsph;
     int32_t nnodes;
@@ -93,7 +94,10 @@ struct DScene {
     float scale;  // CalculateScale(fov) (SceneRenderingHelper.cpp:12-14), host-computed
     float eye[3];
     float bg[3];
-    int32_t max_stack;  // deepest traversal stack any ray can need
+    int32_t max_stack;  // deepest traversal stack any ray can need (LDS stack entries per lane)
+    int32_t lds_bytes;  // bytes of nodes + triangles staged in LDS per workgroup (0 = read from HBM/L2)
+    int32_t dbg;        // ablation switches for profiling only (TPT_DEBUG_FLAGS); 0 in production
+    unsigned long long* dbgc;  // profiling counters (TPT_DEBUG_FLAGS & 2)
 };
 
 }  // namespace tpt

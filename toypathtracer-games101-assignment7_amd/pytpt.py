@@ -11,7 +11,7 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libtpt.so")
+LIB_PATH = os.environ.get("TPT_LIB") or os.path.join(HERE, "libtpt.so")  # TPT_LIB: profiling A/B only
 MODELS_DIR = os.path.join(HERE, "models")
 
 TPT_OK = 0
