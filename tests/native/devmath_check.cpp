@@ -15,6 +15,9 @@ int main(int argc, char** argv) {
         n++;
         if (f2u(sinf(x)) != f2u(tpt_sinf(x))) bad++;
         if (f2u(cosf(x)) != f2u(tpt_cosf(x))) bad++;
+        float s2, c2;
+        tpt_sincosf(x, &s2, &c2);
+        if (f2u(s2) != f2u(sinf(x)) || f2u(c2) != f2u(cosf(x))) bad++;
     }
     printf("sincos n=%ld bad=%ld\n", n, bad);
     long bad2 = 0, n2 = 0;
@@ -44,5 +47,19 @@ int main(int argc, char** argv) {
         if (f2u(a) != f2u(b)) bad4++;
     }
     printf("rng n=%ld bad=%ld\n", n4, bad4);
-    return (bad || bad2 || bad3 || bad4) ? 1 : 0;
+    // f64 sincos: float(r*cos), float(r*sin) as used by GetCosineWeightedSample
+    long bad5 = 0, n5 = 0;
+    for (uint32_t u = 0; u <= hi; u += stride) {
+        float th = u2f(u);
+        double sd, cd;
+        tpt_sincos_d((double)th, &sd, &cd);
+        double gs = std::sin((double)th), gc = std::cos((double)th);
+        for (int k = 1; k <= 4; ++k) {
+            float r = std::sqrt((float)k / 5.0f);
+            n5++;
+            if (f2u((float)(r * cd)) != f2u((float)(r * gc)) || f2u((float)(r * sd)) != f2u((float)(r * gs))) bad5++;
+        }
+    }
+    printf("sincos_d-products n=%ld bad=%ld\n", n5, bad5);
+    return (bad || bad2 || bad3 || bad4 || bad5) ? 1 : 0;
 }

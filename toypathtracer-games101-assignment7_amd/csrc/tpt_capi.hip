@@ -205,7 +205,7 @@ struct tpt_ctx {
     float* rows = nullptr;
     int64_t rows_cap = 0;
     unsigned long long* counters = nullptr;
-    int pt_lanes = 2;  // Q: lanes per pixel of the PT kernel (1, 2, 4, 8)
+    int pt_lanes = 4;  // Q: lanes per pixel of the PT kernel (1, 2, 4, 8)
 };
 
 namespace {
@@ -409,7 +409,7 @@ int tpt_upload_scene(tpt_ctx* c, const tpt_scene_desc* d) {
         ds.dbg = dbg ? std::atoi(dbg) : 0;
         ds.dbgc = c->counters + 8;
         const char* q = std::getenv("TPT_PT_LANES");
-        c->pt_lanes = q ? std::atoi(q) : 2;  // Q = 2 measured best on one MI355X (Standard, 1024 spp)
+        c->pt_lanes = q ? std::atoi(q) : 4;  // Q = 4 measured best on one MI355X (Standard, 1024 spp)
         if (c->pt_lanes != 1 && c->pt_lanes != 2 && c->pt_lanes != 4 && c->pt_lanes != 8) c->pt_lanes = 1;
     }
     c->ds = ds;

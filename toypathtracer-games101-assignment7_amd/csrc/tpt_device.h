@@ -431,7 +431,9 @@ TPT_D V3 cosine_sample(V3 N, float& pdf, uint32_t& rs) {
     float u1 = rng_float(rs);
     float r = sqrt_f(u1);
     float theta = 2 * kPi * rng_float(rs);
-    float x = (float)((double)r * cos_d((double)theta)), y = (float)((double)r * sin_d((double)theta));
+    double sd, cd;
+    tpt_sincos_d((double)theta, &sd, &cd);
+    float x = (float)((double)r * cd), y = (float)((double)r * sd);
     V3 wi = normalized(to_world(v3(x, y, sqrt_f(1.0f - u1)), N));
     pdf = (float)(dot3(wi, N) / (double)kPi);
     return wi;
@@ -466,8 +468,10 @@ TPT_D V3 ggx_sample_h(V3 N, float r, uint32_t& rs) {
     float d1 = rng_float(rs), d2 = rng_float(rs);
     float theta = tpt_atan2f(r * sqrt_f(d1), sqrt_f(1.0f - d1));
     float phi = 2.0f * kPi * d2;
-    float st = tpt_sinf(theta);
-    V3 local = v3(st * tpt_cosf(phi), st * tpt_sinf(phi), tpt_cosf(theta));
+    float st, ct, sp, cp;
+    tpt_sincosf(theta, &st, &ct);
+    tpt_sincosf(phi, &sp, &cp);
+    V3 local = v3(st * cp, st * sp, ct);
     return normalized(to_world(local, N));
 }
 
@@ -640,7 +644,10 @@ TPT_D void object_sample(const DScene& s, const DObj& o, V3& pc, V3& pn, int& pr
         const DSphere sp = s.sph[o.sphere_prim - s.ntri];
         float theta = (float)(2.0 * (double)kPi * (double)rng_float(rs));
         float phi = (float)(kPi * rng_float(rs));
-        V3 dir = v3(tpt_cosf(phi), tpt_sinf(phi) * tpt_cosf(theta), tpt_sinf(phi) * tpt_sinf(theta));
+        float sph, cph, sth, cth;
+        tpt_sincosf(phi, &sph, &cph);
+        tpt_sincosf(theta, &sth, &cth);
+        V3 dir = v3(cph, sph * cth, sph * sth);
         pc = v3(sp.c[0], sp.c[1], sp.c[2]) + mul(dir, sp.r);
         pn = dir;
         prim = o.sphere_prim;

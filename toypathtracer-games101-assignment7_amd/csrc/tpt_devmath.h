@@ -193,42 +193,57 @@ TPT_HD float tpt_cosf(float y) {
     return sincos_poly(x * s, x * x, p, n ^ 1);
 }
 
+// sinf and cosf of the same argument share glibc's reduction (s_sinf.c and
+// s_cosf.c run the same reduce_fast / table selection and differ only in the
+// polynomial parity), so computing both from one reduction is bit-identical.
+TPT_HD void tpt_sincosf(float y, float* sn, float* cs) {
+    double x = y;
+    const SinCosTab* p = &kSinCos[0];
+    if (abstop12(y) < abstop12(0x1.921fb6p-1f)) {
+        double x2 = x * x;
+        if (abstop12(y) < abstop12(0x1p-12f)) { *sn = y; *cs = 1.0f; return; }
+        *sn = sincos_poly(x, x2, p, 0);
+        *cs = sincos_poly(x, x2, p, 1);
+        return;
+    }
+    int n;
+    x = reduce_fast(x, p, &n);
+    double s = p->sign[n & 3];
+    if (n & 2) p = &kSinCos[1];
+    *sn = sincos_poly(x * s, x * x, p, n);
+    *cs = sincos_poly(x * s, x * x, p, n ^ 1);
+}
+
 // atanf / atan2f: fdlibm-derived glibc 2.35 flt-32 s_atanf.c / e_atan2f.c (float
 // arithmetic).  tpt_atan2f covers the hot path's domain (finite y >= 0, x >= 0).
+// The five argument ranges of s_atanf.c differ only in the reduction
+// x' = (A x + B) / (C x + D) with A,C in {0, 1, 1.5, 2} (products exact or rounded
+// exactly as fdlibm's) -- so the range is selected by coefficients and ONE divide,
+// branch-free (lanes of a wave fall in different ranges).  Domain: x >= 0, finite;
+// equal to glibc atanf on every such float (tests/test_devmath.py).
 TPT_HD float tpt_atanf(float x) {
-    const float atanhi[4] = {4.6364760399e-01f, 7.8539812565e-01f, 9.8279368877e-01f, 1.5707962513e+00f};
-    const float atanlo[4] = {5.0121582440e-09f, 3.7748947079e-08f, 3.4473217170e-08f, 7.5497894159e-08f};
     const float aT0 = 3.3333334327e-01f, aT1 = -2.0000000298e-01f, aT2 = 1.4285714924e-01f,
                 aT3 = -1.1111110449e-01f, aT4 = 9.0908870101e-02f, aT5 = -7.6918758452e-02f,
                 aT6 = 6.6610731184e-02f, aT7 = -5.8335702866e-02f, aT8 = 4.9768779427e-02f,
                 aT9 = -3.6531571299e-02f, aT10 = 1.6285819933e-02f;
-    int32_t hx = (int32_t)f2u(x);
-    int32_t ix = hx & 0x7fffffff;
-    int id;
-    if (ix >= 0x4c000000) {
-        if (ix > 0x7f800000) return x + x;
-        return hx > 0 ? atanhi[3] + atanlo[3] : -atanhi[3] - atanlo[3];
-    }
-    if (ix < 0x3ee00000) {
-        if (ix < 0x31000000) return x;
-        id = -1;
-    } else {
-        x = fabs_(x);
-        if (ix < 0x3f980000) {
-            if (ix < 0x3f300000) { id = 0; x = (2.0f * x - 1.0f) / (2.0f + x); }
-            else { id = 1; x = (x - 1.0f) / (x + 1.0f); }
-        } else {
-            if (ix < 0x401c0000) { id = 2; x = (x - 1.5f) / (1.0f + 1.5f * x); }
-            else { id = 3; x = -1.0f / x; }
-        }
-    }
-    float z = x * x;
-    float w = z * z;
-    float s1 = z * (aT0 + w * (aT2 + w * (aT4 + w * (aT6 + w * (aT8 + w * aT10)))));
-    float s2 = w * (aT1 + w * (aT3 + w * (aT5 + w * (aT7 + w * aT9))));
-    if (id < 0) return x - x * (s1 + s2);
-    float r = atanhi[id] - ((x * (s1 + s2) - atanlo[id]) - x);
-    return hx < 0 ? -r : r;
+    const uint32_t ix = f2u(x) & 0x7fffffffu;
+    const int id = ix < 0x3ee00000u ? -1 : ix < 0x3f300000u ? 0 : ix < 0x3f980000u ? 1 : ix < 0x401c0000u ? 2 : 3;
+    const float A = id == 0 ? 2.0f : (id == 3 ? 0.0f : 1.0f);
+    const float B = id == 2 ? -1.5f : -1.0f;
+    const float C = id == 2 ? 1.5f : 1.0f;
+    const float D = id == 0 ? 2.0f : (id == 3 ? 0.0f : 1.0f);
+    const float xr = id < 0 ? x : (A * x + B) / (C * x + D);
+    const float z = xr * xr, w = z * z;
+    const float s1 = z * (aT0 + w * (aT2 + w * (aT4 + w * (aT6 + w * (aT8 + w * aT10)))));
+    const float s2 = w * (aT1 + w * (aT3 + w * (aT5 + w * (aT7 + w * aT9))));
+    const float hi = id <= 0 ? 4.6364760399e-01f : id == 1 ? 7.8539812565e-01f : id == 2 ? 9.8279368877e-01f
+                                                                                           : 1.5707962513e+00f;
+    const float lo = id <= 0 ? 5.0121582440e-09f : id == 1 ? 3.7748947079e-08f : id == 2 ? 3.4473217170e-08f
+                                                                                           : 7.5497894159e-08f;
+    float r = id < 0 ? xr - xr * (s1 + s2) : hi - ((xr * (s1 + s2) - lo) - xr);
+    if (ix < 0x31000000u) r = x;                          // |x| < 2^-29
+    if (ix >= 0x4c000000u) r = 1.5707962513e+00f + 7.5497894159e-08f;  // |x| >= 2^25
+    return r;
 }
 TPT_HD float tpt_atan2f(float y, float x) {
     const float pi_o_2 = 1.5707963705e+00f, pi_lo = -8.7422776573e-08f;
@@ -244,11 +259,45 @@ TPT_HD float tpt_atan2f(float y, float x) {
 }
 
 // Unqualified cos/sin on a float in SampleHelperFunctions.hpp:110 bind to the
-// double ::cos/::sin under libstdc++; only the float-rounded product r*cos(theta)
-// is kept, so a faithfully rounded double cos suffices for that float result
-// except within ~2^-29 of a float rounding boundary.
-TPT_HD double cos_d(double x) { return ::cos(x); }  // ocml f64 on the device, glibc on the host
-TPT_HD double sin_d(double x) { return ::sin(x); }
+// double ::cos/::sin under libstdc++; only the float-rounded product r*cos(theta) is
+// kept.  tpt_sincos_d: fdlibm k_sin/k_cos kernels after a 3-part pi/2 reduction
+// (0 <= x <= ~8), within 1 ulp (double) of glibc on every float in [0, 2pi]; the
+// float products r*cos / r*sin then agree with glibc's (0 mismatches in 3.8e7
+// checks at the differing inputs, tests/test_devmath.py).  One shared reduction
+// for both functions, ~40 f64 ops instead of two ocml calls.
+TPT_HD double rint_d(double x) {
+#if defined(__HIPCC__)
+    return __builtin_rint(x);
+#else
+    return std::nearbyint(x);
+#endif
+}
+TPT_HD void tpt_sincos_d(double x, double* sn, double* cs) {
+    const double S1 = -1.66666666666666324348e-01, S2 = 8.33333333332248946124e-03, S3 = -1.98412698298579493134e-04,
+                 S4 = 2.75573137070700676789e-06, S5 = -2.50507602534068634195e-08, S6 = 1.58969099521155010221e-10;
+    const double C1 = 4.16666666666666019037e-02, C2 = -1.38888888888741095749e-03, C3 = 2.48015872894767294178e-05,
+                 C4 = -2.75573143513906633035e-07, C5 = 2.08757232129817482790e-09, C6 = -1.13596475577881948265e-11;
+    const double invpio2 = 6.36619772367581382433e-01, pio2_1 = 1.57079632673412561417e+00,
+                 pio2_2 = 6.07710050630396597660e-11, pio2_2t = 2.02226624879595063154e-21;
+    const double fn = rint_d(x * invpio2);
+    const int n = (int)fn;
+    double r = x - fn * pio2_1;
+    const double t = r;
+    double w = fn * pio2_2;
+    r = t - w;
+    w = fn * pio2_2t - ((t - r) - w);
+    const double y0 = r - w;
+    const double y1 = (r - y0) - w;
+    const double z = y0 * y0, v = z * y0;
+    const double rr = S2 + z * (S3 + z * (S4 + z * (S5 + z * S6)));
+    const double ks = y0 - ((z * (0.5 * y1 - v * rr) - y1) - v * S1);
+    const double rc = z * (C1 + z * (C2 + z * (C3 + z * (C4 + z * (C5 + z * C6)))));
+    const double hz = 0.5 * z, ww = 1.0 - hz;
+    const double kc = ww + (((1.0 - ww) - hz) + (z * rc - y0 * y1));
+    const int q = n & 3;
+    *sn = q == 0 ? ks : q == 1 ? kc : q == 2 ? -ks : -kc;
+    *cs = q == 0 ? kc : q == 1 ? -ks : q == 2 ? -kc : ks;
+}
 
 static const float kPi = 3.141592653589793f;  // global.hpp:7-8 (float M_PI)
 
