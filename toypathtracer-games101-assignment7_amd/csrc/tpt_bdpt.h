@@ -15,6 +15,12 @@
 //    right after Material::sample; SampleNextVertex's intersection and BSDF
 //    evaluation draw nothing, so they are skipped when the RR draw ends the path
 //    and the BSDF evaluation is skipped when the pdf test ends it.
+//    For k >= 2 the factor folded into cur_pdf is safe_div(rev * rr, pdf) with rr
+//    either 1 or .8, so both variants are precomputed per vertex (`q1`, `q8`): the
+//    O(n^3) chain then costs a select and a multiply per step, same float ops in the
+//    same order.
+//  * Rays are traced as wave packets (tpt_device.h: traverse_packet /
+//    shadow_pts_packet).
 //  * The camera vertex v1 is the same for every sample (no jitter) and is hoisted
 //    out of the spp loop.
 //  * t = 1 splats (DrawToImage, SceneRenderingHelper.cpp:30-55) are fp32 atomics;
@@ -35,7 +41,7 @@ struct BVert {
     int type, prim;
     float pdf;
     V3 alpha;
-    float rev;
+    float q1, q8;  // safe_div(rev * rr, pdf) for rr = 1 and rr = .8 (rev: reverse pdf)
 };
 
 TPT_D PTV as_ptv(const BVert& b) {
@@ -85,19 +91,26 @@ TPT_D float prim_pdf(const DScene& s, int prim) {
 }
 
 // Scene::ShadowCheck(const PTVertex&, const PTVertex&) (Scene.cpp:50-83)
-TPT_D bool shadow_v(const DScene& s, const BVert& v1, const BVert& v2, int* stk) {
+template <bool kPacket>
+TPT_D bool shadow_v(const DScene& s, const BVert& v1, const BVert& v2, Packet pk, int* stk) {
     V3 atob = v2.x - v1.x;
+    bool test = true;
+    int cull = TPT_CULL_BACK;
     if (v1.prim >= 0 && v2.prim != v1.prim && s.mats[prim_mat(s, v1.prim)].type == TPT_TRANSPARENT) {
-        if (dot3(atob, v1.N) < 0.0f) return shadow_pts(s, v1.x, v2.x, TPT_CULL_FRONT, stk);
-        return shadow_pts(s, v1.x, v2.x, TPT_CULL_BACK, stk);
+        if (dot3(atob, v1.N) < 0.0f) cull = TPT_CULL_FRONT;
+    } else if (v1.prim >= 0 && dot3(atob, v1.N) < 0.0f) {
+        test = false;  // fast path "not shadowed" (Scene.cpp:71-74)
+    } else if (v2.prim >= 0 && dot3(-atob, v2.N) < 0.0f) {
+        test = false;  // Scene.cpp:75-78
     }
-    if (v1.prim >= 0 && dot3(atob, v1.N) < 0.0f) return false;
-    if (v2.prim >= 0 && dot3(-atob, v2.N) < 0.0f) return false;
-    return shadow_pts(s, v1.x, v2.x, TPT_CULL_BACK, stk);
+    bool sh = false;
+    if (test) sh = kPacket ? shadow_pts_packet(s, v1.x, v2.x, cull, pk) : shadow_pts(s, v1.x, v2.x, cull, stk);
+    return sh;
 }
 
 // FillPathUsingRussianRoulette (BDPT.cpp:92-118) + SampleNextVertex (:261-279).
-TPT_D int fill_path(const DScene& s, BVert* P, int start, uint32_t& rs, int* stk) {
+template <bool kPacket>
+TPT_D int fill_path(const DScene& s, BVert* P, int start, uint32_t& rs, Packet pk, int* stk) {
     int count = start + 1;
     for (int i = start; i < kMaxLen - 1; i++) {
         BVert cur = P[i];
@@ -110,7 +123,9 @@ TPT_D int fill_path(const DScene& s, BVert* P, int start, uint32_t& rs, int* stk
         if (rng_float(rs) > rr) break;
         float ct = (float)dabs_(dot3(cur.N, wi));
         float sr = safe_div(raw, ct);
-        PTV it = scene_intersect(s, make_ray(cur.x, wi), dot3(cur.N, wi) > 0.0f ? TPT_CULL_BACK : TPT_CULL_FRONT, stk);
+        const Ray nr = make_ray(cur.x, wi);
+        const int cl = dot3(cur.N, wi) > 0.0f ? TPT_CULL_BACK : TPT_CULL_FRONT;
+        PTV it = kPacket ? scene_intersect_packet(s, nr, cl, pk) : scene_intersect(s, nr, cl, stk);
         float pdf = srpdf_to_area(sr, cur.type, cur.x, cur.N, it.type, it.x, it.N);
         if (pdf == 0.0f) break;
         V3 bsdf = eval_bsdf(m, wo, wi, cur.N, false);
@@ -118,41 +133,49 @@ TPT_D int fill_path(const DScene& s, BVert* P, int start, uint32_t& rs, int* stk
         nx.x = it.x; nx.N = it.N; nx.type = it.type; nx.prim = it.prim;
         nx.pdf = pdf * rr;
         nx.alpha = divs(cur.alpha * safe_div(bsdf, sr), rr);
-        nx.rev = 0.0f;
+        nx.q1 = nx.q8 = 0.0f;
         P[i + 1] = nx;
         count++;
     }
     return count;
 }
 
-// Reverse pdfs of vertices j = 0..count-3 (Append with last = j+1, Pre = j+2).
+// Reverse pdfs of vertices j = 0..count-3 (Append with last = j+1, Pre = j+2),
+// folded into the two possible cur_pdf factors safe_div(rev * rr, pdf_j).
 TPT_D void path_rev(const DScene& s, BVert* P, int count) {
     for (int j = 0; j + 2 < count; ++j) {
         const BVert& a = P[j + 1];
-        P[j].rev = append_pdf(s, a.type, a.prim, a.x, a.N, P[j + 2].x, P[j].type, P[j].x, P[j].N);
+        const float rev = append_pdf(s, a.type, a.prim, a.x, a.N, P[j + 2].x, P[j].type, P[j].x, P[j].N);
+        P[j].q1 = safe_div(rev * 1.f, P[j].pdf);
+        P[j].q8 = safe_div(rev * .8f, P[j].pdf);
     }
 }
 
 // BDPTPath::PathWeight (BDPT.cpp:173-259) for light sub-length sl, camera sub-length tl.
-TPT_D V3 path_weight(const DScene& s, const BVert* L, int sl, const BVert* C, int tl, int* stk) {
+// Paths are read through an accessor P: P::cam(j), P::lit(j) return vertex records,
+// P::camq / P::litq the cached MIS factors (rr .8 when `r8`).
+template <class P, bool kPacket>
+TPT_D V3 path_weight(const DScene& s, const P& paths, int sl, int tl, Packet pk, int* stk) {
     const int z = tl - 1;
-    const BVert cz = C[z];
+    const BVert cz = paths.cam(z);
     if (cz.type == T_BG) return sl == 0 ? cz.alpha * v3(s.bg[0], s.bg[1], s.bg[2]) : v3s(0.0f);
-    if (sl != 0 && L[sl - 1].type == T_BG) return v3s(0.0f);
+    const BVert ly = sl >= 1 ? paths.lit(sl - 1) : cz;
+    if (sl != 0 && ly.type == T_BG) return v3s(0.0f);
+    const V3 cpre = z >= 1 ? paths.cam(z - 1).x : cz.x;
+    const V3 lpre = sl >= 2 ? paths.lit(sl - 2).x : ly.x;
     V3 cst;
     if (sl == 0) {
-        V3 wi = normalized(C[z - 1].x - cz.x);
+        V3 wi = normalized(cpre - cz.x);
         V3 em = v3s(0.0f);  // PathVertex::Emission (BDPT.hpp:119-128)
         if (cz.prim >= 0) em = load_mat(s, prim_mat(s, cz.prim)).em;
         cst = mul(em, (float)dot3(normal_of(cz.type, cz.N), wi));
         if (dot3(em, em) == 0.0f) return v3s(0.0f);
     } else {
-        const BVert ly = L[sl - 1];
         float d2;
         V3 dir = normalize_len2(cz.x - ly.x, &d2);
-        if (shadow_v(s, cz, ly, stk)) return v3s(0.0f);
-        V3 fl = eval_bsdf_sa(s, ly.type, ly.prim, ly.x, ly.N, sl >= 2 ? L[sl - 2].x : ly.x, dir);
-        V3 fc = eval_bsdf_sa(s, cz.type, cz.prim, cz.x, cz.N, z >= 1 ? C[z - 1].x : cz.x, -dir);
+        if (shadow_v<kPacket>(s, cz, ly, pk, stk)) return v3s(0.0f);
+        V3 fl = eval_bsdf_sa(s, ly.type, ly.prim, ly.x, ly.N, lpre, dir);
+        V3 fc = eval_bsdf_sa(s, cz.type, cz.prim, cz.x, cz.N, cpre, -dir);
         cst = mul(fl * fc, (float)dabs_(dot3(normal_of(ly.type, ly.N), dir) * dot3(normal_of(cz.type, cz.N), -dir) / (double)d2));
     }
     float wd = 1.0f;
@@ -160,15 +183,16 @@ TPT_D V3 path_weight(const DScene& s, const BVert* L, int sl, const BVert* C, in
     float cur = 1.0f;
     for (int k = 0; k < sl; ++k) {
         const int j = sl - 1 - k;
-        const BVert v = L[j];
-        float pdf;
-        if (k == 0) pdf = append_pdf(s, cz.type, cz.prim, cz.x, cz.N, z >= 1 ? C[z - 1].x : cz.x, v.type, v.x, v.N);
-        else if (k == 1) {
-            const BVert a = L[sl - 1];
-            pdf = append_pdf(s, a.type, a.prim, a.x, a.N, cz.x, v.type, v.x, v.N);
-        } else pdf = v.rev;
-        pdf *= rr_of(tl + k);
-        cur *= safe_div(pdf, v.pdf);
+        if (k >= 2) {
+            cur *= paths.litq(j, tl + k > 4);
+        } else {
+            const BVert v = k == 0 ? ly : paths.lit(j);
+            float pdf;
+            if (k == 0) pdf = append_pdf(s, cz.type, cz.prim, cz.x, cz.N, cpre, v.type, v.x, v.N);
+            else pdf = append_pdf(s, ly.type, ly.prim, ly.x, ly.N, cz.x, v.type, v.x, v.N);
+            pdf *= rr_of(tl + k);
+            cur *= safe_div(pdf, v.pdf);
+        }
         wd += cur * cur;
         if (cur == 0.0f) break;
     }
@@ -176,29 +200,30 @@ TPT_D V3 path_weight(const DScene& s, const BVert* L, int sl, const BVert* C, in
     cur = 1.0f;
     for (int k = 0; k < tl; ++k) {
         const int j = tl - 1 - k;
-        const BVert v = C[j];
         const int count = sl + k;
-        float pdf;
-        if (count == 0) {
-            pdf = prim_pdf(s, v.prim);  // Append(count==0): vertex.obj->pdf(), no RR factor
+        if (k >= 2) {
+            cur *= paths.camq(j, count > 4);
         } else {
-            if (k == 0) {
-                const BVert a = L[sl - 1];
-                pdf = append_pdf(s, a.type, a.prim, a.x, a.N, sl >= 2 ? L[sl - 2].x : a.x, v.type, v.x, v.N);
-            } else if (k == 1) {
-                // last = C[tl-1] as appended (type Light when it opened the path, BDPT.cpp:240-242)
-                const int at = sl == 0 ? T_LIGHT : cz.type;
-                pdf = append_pdf(s, at, cz.prim, cz.x, cz.N, sl >= 1 ? L[sl - 1].x : cz.x, v.type, v.x, v.N);
+            const BVert v = k == 0 ? cz : paths.cam(j);
+            float pdf;
+            if (count == 0) {
+                pdf = prim_pdf(s, v.prim);  // Append(count==0): vertex.obj->pdf(), no RR factor
             } else {
-                pdf = v.rev;
+                if (k == 0) {
+                    pdf = append_pdf(s, ly.type, ly.prim, ly.x, ly.N, lpre, v.type, v.x, v.N);
+                } else {
+                    // last = C[tl-1] as appended (type Light when it opened the path, BDPT.cpp:240-242)
+                    const int at = sl == 0 ? T_LIGHT : cz.type;
+                    pdf = append_pdf(s, at, cz.prim, cz.x, cz.N, sl >= 1 ? ly.x : cz.x, v.type, v.x, v.N);
+                }
+                pdf *= rr_of(count);
             }
-            pdf *= rr_of(count);
+            cur *= safe_div(pdf, v.pdf);
         }
-        cur *= safe_div(pdf, v.pdf);
         wd += cur * cur;
         if (cur == 0.0f) break;
     }
-    V3 lt = sl == 0 ? v3s(1.0f) : L[sl - 1].alpha;
+    V3 lt = sl == 0 ? v3s(1.0f) : ly.alpha;
     V3 uc = lt * cz.alpha * cst;
     return divs(uc, wd);
 }
@@ -226,74 +251,160 @@ TPT_D void splat_add(const DScene& s, V3 light, V3 cam, V3 value, float* splat) 
         }
 }
 
-// One pixel stream: Renderer.cpp:42-52 with BDPT (BDPT.cpp:282-315).
-TPT_D void bdpt_pixel(const DScene& s, int64_t i, int spp, V3& acc, float* splat, unsigned long long& nbounce,
-                      int* stk) {
-    BVert C[kMaxLen], L[kMaxLen];
+struct PrivPaths {  // paths held in the lane's private arrays
+    const BVert* L;
+    const BVert* C;
+    TPT_D BVert cam(int j) const { return C[j]; }
+    TPT_D BVert lit(int j) const { return L[j]; }
+    TPT_D float camq(int j, bool r8) const { return r8 ? C[j].q8 : C[j].q1; }
+    TPT_D float litq(int j, bool r8) const { return r8 ? L[j].q8 : L[j].q1; }
+};
+
+// GenerateCameraPath's v0/v1 (BDPT.cpp:41-59): identical for every sample of a pixel.
+TPT_D void camera_vertices(const DScene& s, int64_t i, BVert& c0, BVert& c1, int* stk) {
     const int px = (int)(i % s.width), py = (int)(i / s.width);
     const V3 dir = pixel_ray(px, py, s.width, s.height, s.scale);
     const V3 eye = v3(s.eye[0], s.eye[1], s.eye[2]);
-    const Ray cray = make_ray(eye, dir);
-    // GenerateCameraPath (BDPT.cpp:41-59): v0, v1 identical for every sample
-    BVert c0;
     c0.x = eye; c0.N = v3s(0.0f); c0.type = T_CAM; c0.prim = -1;
-    c0.pdf = kCamZeroPdf; c0.alpha = v3s(1.0f); c0.rev = 0.0f;
-    PTV h1 = scene_intersect(s, cray, TPT_CULL_BACK, stk);
-    BVert c1;
+    c0.pdf = kCamZeroPdf; c0.alpha = v3s(1.0f); c0.q1 = c0.q8 = 0.0f;
+    PTV h1 = scene_intersect(s, make_ray(eye, dir), TPT_CULL_BACK, stk);
     c1.x = h1.x; c1.N = h1.N; c1.type = h1.type; c1.prim = h1.prim;
     c1.pdf = srpdf_to_area(kCamRayPdf, T_CAM, c0.x, c0.N, h1.type, h1.x, h1.N);
     c1.alpha = v3s(1.0f);
-    c1.rev = 0.0f;
+    c1.q1 = c1.q8 = 0.0f;
+}
+
+// One BDPT sample's subpaths (BDPT.cpp:286-287) and their cached MIS factors.
+template <bool kPacket>
+TPT_D void generate_paths(const DScene& s, const BVert& c0, const BVert& c1, uint32_t& rs, BVert* C, BVert* L,
+                          int& cn, int& ln, Packet pk, int* stk) {
+    C[0] = c0;
+    C[1] = c1;
+    cn = 2;
+    if (c1.type != T_BG) cn = fill_path<kPacket>(s, C, 1, rs, pk, stk);
+    // GenerateLightPath (BDPT.cpp:61-90) from m_emissionObjects[0]
     const DObj lo = s.objs[s.emitters[0]];
     const V3 lem = load_mat(s, lo.mat).em;
+    V3 pc, pn;
+    int pp;
+    object_sample(s, lo, pc, pn, pp, rs);
+    BVert l0;
+    l0.x = pc; l0.N = pn; l0.type = T_LIGHT; l0.prim = pp;
+    l0.pdf = lo.pdf;
+    l0.alpha = divs(lem, l0.pdf);
+    l0.q1 = l0.q8 = 0.0f;
+    float pdf1;
+    V3 wi = cosine_sample(pn, pdf1, rs);
+    float ct = (float)dot3(l0.N, wi);
+    pdf1 = safe_div(pdf1, ct);
+    const Ray lr = make_ray(l0.x, wi);
+    PTV it = kPacket ? scene_intersect_packet(s, lr, TPT_CULL_BACK, pk) : scene_intersect(s, lr, TPT_CULL_BACK, stk);
+    BVert l1;
+    l1.x = it.x; l1.N = it.N; l1.type = it.type; l1.prim = it.prim;
+    l1.pdf = srpdf_to_area(pdf1, T_LIGHT, l0.x, l0.N, it.type, it.x, it.N);
+    l1.alpha = v3s(0.0f);  // fresh InternalPathVertex (BDPT.hpp:19)
+    l1.q1 = l1.q8 = 0.0f;
+    L[0] = l0;
+    if (pdf1 != 0.0f) l1.alpha = safe_div(l0.alpha, pdf1);
+    L[1] = l1;
+    if (pdf1 == 0.0f && it.type == T_BG) ln = 2;
+    else ln = fill_path<kPacket>(s, L, 1, rs, pk, stk);
+    path_rev(s, C, cn);
+    path_rev(s, L, ln);
+}
+
+// One pixel stream, all strategies in one lane (Renderer.cpp:42-52 with BDPT,
+// BDPT.cpp:282-315).  Used for short pixel lists; full frames use the wavefront
+// kernels (tpt_capi.hip), which balance strategies across lanes.
+template <bool kPacket>
+TPT_D void bdpt_pixel(const DScene& s, int64_t i, int spp, V3& acc, float* splat, unsigned long long& nbounce,
+                      Packet pk, int* stk) {
+    BVert C[kMaxLen], L[kMaxLen];
+    BVert c0, c1;
+    camera_vertices(s, i, c0, c1, stk);
     const float inv = 1.0f / spp;
     uint32_t rs = (uint32_t)((int)i + 1);
     acc = v3s(0.0f);
+    PrivPaths paths;
+    paths.L = L;
+    paths.C = C;
     for (int sp = 0; sp < spp; ++sp) {
-        C[0] = c0;
-        C[1] = c1;
-        int cn = 2;
-        if (c1.type != T_BG) cn = fill_path(s, C, 1, rs, stk);
-        // GenerateLightPath (BDPT.cpp:61-90) from m_emissionObjects[0]
-        int ln;
-        {
-            V3 pc, pn;
-            int pp;
-            object_sample(s, lo, pc, pn, pp, rs);
-            BVert l0;
-            l0.x = pc; l0.N = pn; l0.type = T_LIGHT; l0.prim = pp;
-            l0.pdf = lo.pdf;
-            l0.alpha = divs(lem, l0.pdf);
-            l0.rev = 0.0f;
-            float pdf1;
-            V3 wi = cosine_sample(pn, pdf1, rs);
-            float ct = (float)dot3(l0.N, wi);
-            pdf1 = safe_div(pdf1, ct);
-            PTV it = scene_intersect(s, make_ray(l0.x, wi), TPT_CULL_BACK, stk);
-            BVert l1;
-            l1.x = it.x; l1.N = it.N; l1.type = it.type; l1.prim = it.prim;
-            l1.pdf = srpdf_to_area(pdf1, T_LIGHT, l0.x, l0.N, it.type, it.x, it.N);
-            l1.alpha = v3s(0.0f);  // fresh InternalPathVertex (BDPT.hpp:19)
-            l1.rev = 0.0f;
-            L[0] = l0;
-            if (pdf1 != 0.0f) l1.alpha = safe_div(l0.alpha, pdf1);
-            L[1] = l1;
-            if (pdf1 == 0.0f && it.type == T_BG) ln = 2;
-            else ln = fill_path(s, L, 1, rs, stk);
-        }
+        int cn, ln;
+        generate_paths<kPacket>(s, c0, c1, rs, C, L, cn, ln, pk, stk);
         nbounce += (unsigned long long)(cn + ln);
-        path_rev(s, C, cn);
-        path_rev(s, L, ln);
         V3 res = v3s(0.0f);
-        for (int t = 1; t <= cn; ++t)
-            for (int sl = 0; sl <= ln; ++sl) {
-                if (t + sl < 2) continue;
-                V3 w = vmax0(path_weight(s, L, sl, C, t, stk));
-                if (t > 1) res = res + w;
-                else if (splat) splat_add(s, L[sl - 1].x, C[0].x, w, splat);
-            }
+        // (t, s) strategies in the reference's order (t outer, s inner); pi = 0 is
+        // (t=1, s=0): t + s < 2, skipped.
+        const int np = cn * (ln + 1);
+        for (int pi = 1; pi < np; ++pi) {
+            const int t = pi / (ln + 1) + 1, sl = pi % (ln + 1);
+            V3 w = vmax0(path_weight<PrivPaths, kPacket>(s, paths, sl, t, pk, stk));
+            if (t > 1) res = res + w;
+            else if (splat) splat_add(s, L[sl - 1].x, C[0].x, w, splat);
+        }
         acc = acc + mul(res, inv);
     }
 }
+
+// ------------------------------------------------------------ wavefront --
+// Per sample iteration, for every pixel of the shard:
+//   gen:     generate both subpaths (RNG-sequential per pixel) and write them to
+//            HBM as SoA records [path*16+vertex][field][pixel];
+//   scan:    inclusive prefix sum of the strategy counts cn*(ln+1)-1;
+//   scatter: owner[g] = pixel for every strategy g;
+//   connect: ONE LANE PER STRATEGY (PathWeight), so a wave's work is 64 strategies
+//            instead of the longest lane's cn*(ln+1) (measured 18 mean vs 73 max);
+//            t = 1 splats go straight to the splat buffer;
+//   fold:    per pixel, result += w over its strategies in (t, s) order (t > 1) and
+//            fb += (1/spp) * result -- the reference's summation order.
+constexpr int kRecF = 13;  // x(3) N(3) type|prim pdf alpha(3) q1 q8
+struct WfState {
+    float* rec;           // 32 * kRecF * n floats
+    int* cnt;             // cn | ln << 16
+    int* np;              // strategies per pixel
+    int* incl;            // inclusive scan of np
+    int* owner;           // strategy -> pixel
+    float* res;           // 3 floats per strategy
+    uint32_t* rng;        // XorShift state per pixel stream
+    float* acc;           // 3 floats per pixel
+    const int64_t* list;  // pixel list (or null: begin + k*stride)
+    int64_t begin, stride, n;
+    unsigned long long* bounces;
+};
+TPT_D int64_t wf_pixel(const WfState& w, int64_t k) { return w.list ? w.list[k] : w.begin + k * w.stride; }
+TPT_D int tp_pack(int type, int prim) { return (prim + 1) * 4 + type; }
+TPT_D void rec_store(const WfState& w, int slot, int64_t k, const BVert& v) {
+    float* r = w.rec + (int64_t)slot * kRecF * w.n + k;
+    const int64_t n = w.n;
+    r[0 * n] = v.x.x; r[1 * n] = v.x.y; r[2 * n] = v.x.z;
+    r[3 * n] = v.N.x; r[4 * n] = v.N.y; r[5 * n] = v.N.z;
+    r[6 * n] = __builtin_bit_cast(float, tp_pack(v.type, v.prim));
+    r[7 * n] = v.pdf;
+    r[8 * n] = v.alpha.x; r[9 * n] = v.alpha.y; r[10 * n] = v.alpha.z;
+    r[11 * n] = v.q1; r[12 * n] = v.q8;
+}
+struct GlobPaths {  // one pixel's paths in the HBM records
+    const float* rec;
+    int64_t n, k;
+    TPT_D BVert load(int slot) const {
+        const float* r = rec + (int64_t)slot * kRecF * n + k;
+        BVert v;
+        v.x = v3(r[0 * n], r[1 * n], r[2 * n]);
+        v.N = v3(r[3 * n], r[4 * n], r[5 * n]);
+        const int tp = __builtin_bit_cast(int, r[6 * n]);
+        v.type = tp & 3;
+        v.prim = (tp >> 2) - 1;
+        v.pdf = r[7 * n];
+        v.alpha = v3(r[8 * n], r[9 * n], r[10 * n]);
+        v.q1 = r[11 * n];
+        v.q8 = r[12 * n];
+        return v;
+    }
+    TPT_D float q(int slot, bool r8) const { return rec[((int64_t)slot * kRecF + (r8 ? 12 : 11)) * n + k]; }
+    TPT_D BVert cam(int j) const { return load(j); }
+    TPT_D BVert lit(int j) const { return load(kMaxLen + j); }
+    TPT_D float camq(int j, bool r8) const { return q(j, r8); }
+    TPT_D float litq(int j, bool r8) const { return q(kMaxLen + j, r8); }
+};
 
 }  // namespace tpt

@@ -6,6 +6,7 @@
 // 9,604 wave64s).  PT's draws per sample do not, so PT spreads a pixel's samples
 // over Q lanes (see tpt_pt_kernel).
 #include <hip/hip_runtime.h>
+#include <rocprim/device/device_scan.hpp>
 
 #include <algorithm>
 #include <chrono>
@@ -153,17 +154,100 @@ __global__ __launch_bounds__(kBlock) void tpt_bdpt_kernel(DScene s, int spp, int
                                                           float* __restrict__ out, float* __restrict__ splat,
                                                           unsigned long long* __restrict__ bounces) {
     int* stk = stage_scene<kLds>(s);
+    TPT_PACKET_DECL
     const int64_t k = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (k >= count) return;
     const int64_t i = list ? list[k] : begin + k * stride;
     const int64_t row = list ? k : i;
     V3 acc = v3s(0.0f);
     unsigned long long nb = 0;
-    bdpt_pixel(s, i, spp, acc, splat, nb, stk);
+    bdpt_pixel<false>(s, i, spp, acc, splat, nb, pk, stk);
     out[3 * row + 0] = acc.x;
     out[3 * row + 1] = acc.y;
     out[3 * row + 2] = acc.z;
     if (bounces) atomicAdd(bounces, nb);
+}
+
+// ---- wavefront BDPT kernels (see tpt_bdpt.h, "wavefront") --------------------
+template <bool kLds>
+__global__ __launch_bounds__(kBlock) void tpt_bdpt_gen_kernel(DScene s, WfState w, int first) {
+    int* stk = stage_scene<kLds>(s);
+    TPT_PACKET_DECL
+    const int64_t k = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (k >= w.n) return;
+    const int64_t i = wf_pixel(w, k);
+    BVert C[kMaxLen], L[kMaxLen], c0, c1;
+    camera_vertices(s, i, c0, c1, stk);
+    uint32_t rs = first ? (uint32_t)((int)i + 1) : w.rng[k];  // ResetRandom(i + 1), Renderer.cpp:42
+    if (first) { w.acc[3 * k] = 0.0f; w.acc[3 * k + 1] = 0.0f; w.acc[3 * k + 2] = 0.0f; }
+    int cn, ln;
+    generate_paths<false>(s, c0, c1, rs, C, L, cn, ln, pk, stk);
+    w.rng[k] = rs;
+    for (int j = 0; j < cn; ++j) rec_store(w, j, k, C[j]);
+    for (int j = 0; j < ln; ++j) rec_store(w, kMaxLen + j, k, L[j]);
+    w.cnt[k] = cn | (ln << 16);
+    w.np[k] = cn * (ln + 1) - 1;
+    atomicAdd(w.bounces, (unsigned long long)(cn + ln));
+}
+
+__global__ __launch_bounds__(kBlock) void tpt_bdpt_scatter_kernel(WfState w) {
+    const int64_t k = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (k >= w.n) return;
+    const int e = w.incl[k], b = e - w.np[k];
+    for (int g = b; g < e; ++g) w.owner[g] = (int)k;
+}
+
+template <bool kLds>
+__global__ __launch_bounds__(kBlock) void tpt_bdpt_conn_kernel(DScene s, WfState w, float* __restrict__ splat) {
+    int* stk = stage_scene<kLds>(s);
+    TPT_PACKET_DECL
+    const int64_t total = w.incl[w.n - 1];
+    const V3 eye = v3(s.eye[0], s.eye[1], s.eye[2]);
+    for (int64_t g = (int64_t)blockIdx.x * kBlock + threadIdx.x; g < total; g += (int64_t)gridDim.x * kBlock) {
+        const int k = w.owner[g];
+        const int b = w.incl[k] - w.np[k];
+        const int pi = (int)(g - b) + 1;  // strategy index in (t, s) order; pi = 0 skipped
+        const int ln = w.cnt[k] >> 16;
+        const int t = pi / (ln + 1) + 1, sl = pi % (ln + 1);
+        GlobPaths P;
+        P.rec = w.rec;
+        P.n = w.n;
+        P.k = k;
+        const V3 v = vmax0(path_weight<GlobPaths, false>(s, P, sl, t, pk, stk));
+        if (t > 1) {
+            w.res[3 * g] = v.x;
+            w.res[3 * g + 1] = v.y;
+            w.res[3 * g + 2] = v.z;
+        } else if (splat) {
+            splat_add(s, P.lit(sl - 1).x, eye, v, splat);
+        }
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void tpt_bdpt_fold_kernel(WfState w, float inv) {
+    const int64_t k = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (k >= w.n) return;
+    const int e = w.incl[k], b = e - w.np[k];
+    const int ln = w.cnt[k] >> 16;
+    V3 res = v3s(0.0f);  // BDPT.cpp:289 `Vector3f result;`
+    for (int g = b; g < e; ++g) {
+        const int pi = g - b + 1;
+        if (pi / (ln + 1) + 1 > 1) res = res + v3(w.res[3 * g], w.res[3 * g + 1], w.res[3 * g + 2]);
+    }
+    V3 acc = v3(w.acc[3 * k], w.acc[3 * k + 1], w.acc[3 * k + 2]);
+    acc = acc + mul(res, inv);  // Renderer.cpp:49 `fb[i] += (1.0f / spp) * BDPT(...)`
+    w.acc[3 * k] = acc.x;
+    w.acc[3 * k + 1] = acc.y;
+    w.acc[3 * k + 2] = acc.z;
+}
+
+__global__ __launch_bounds__(kBlock) void tpt_bdpt_out_kernel(WfState w, float* __restrict__ out, int rows) {
+    const int64_t k = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (k >= w.n) return;
+    const int64_t row = rows ? k : wf_pixel(w, k);
+    out[3 * row] = w.acc[3 * k];
+    out[3 * row + 1] = w.acc[3 * k + 1];
+    out[3 * row + 2] = w.acc[3 * k + 2];
 }
 
 __global__ void tpt_scale_kernel(float* __restrict__ buf, int64_t n, float spp) {
@@ -206,6 +290,13 @@ struct tpt_ctx {
     int64_t rows_cap = 0;
     unsigned long long* counters = nullptr;
     int pt_lanes = 4;  // Q: lanes per pixel of the PT kernel (1, 2, 4, 8)
+    // wavefront BDPT state (sized for wf_cap pixels)
+    void* wf_mem = nullptr;
+    int64_t wf_cap = 0;
+    WfState wf{};
+    void* scan_tmp = nullptr;
+    size_t scan_bytes = 0;
+    bool bdpt_mono = false;  // TPT_BDPT_KERNEL=mono: one lane per pixel stream (A/B only)
 };
 
 namespace {
@@ -248,6 +339,38 @@ int ensure_fb(tpt_ctx* c) {
     return TPT_OK;
 }
 
+// Wavefront BDPT buffers for n pixel streams: path records (1.7 KB / pixel) and the
+// strategy list (<= 271 strategies / pixel: cn, ln <= 16).
+int ensure_wf(tpt_ctx* c, int64_t n) {
+    if (n <= c->wf_cap) return TPT_OK;
+    if (c->wf_mem) (void)hipFree(c->wf_mem);
+    if (c->scan_tmp) (void)hipFree(c->scan_tmp);
+    c->wf_mem = c->scan_tmp = nullptr;
+    c->wf_cap = 0;
+    const int64_t maxs = (int64_t)kMaxLen * (kMaxLen + 1) - 1;
+    auto al = [](int64_t b) { return (b + 255) & ~(int64_t)255; };
+    const int64_t b_rec = al(2 * kMaxLen * kRecF * n * 4), b_i = al(n * 4), b_own = al(n * maxs * 4),
+                  b_res = al(n * maxs * 12), b_acc = al(n * 12);
+    const int64_t total = b_rec + 4 * b_i + b_own + b_res + b_acc;
+    HIP_TRY(c, hipMalloc(&c->wf_mem, total));
+    char* p = (char*)c->wf_mem;
+    WfState& w = c->wf;
+    w.rec = (float*)p; p += b_rec;
+    w.cnt = (int*)p; p += b_i;
+    w.np = (int*)p; p += b_i;
+    w.incl = (int*)p; p += b_i;
+    w.rng = (uint32_t*)p; p += b_i;
+    w.owner = (int*)p; p += b_own;
+    w.res = (float*)p; p += b_res;
+    w.acc = (float*)p;
+    size_t bytes = 0;
+    HIP_TRY(c, rocprim::inclusive_scan(nullptr, bytes, w.np, w.incl, (size_t)n, rocprim::plus<int>(), c->stream));
+    HIP_TRY(c, hipMalloc(&c->scan_tmp, bytes));
+    c->scan_bytes = bytes;
+    c->wf_cap = n;
+    return TPT_OK;
+}
+
 int64_t shard_count(int64_t npix, int64_t begin, int64_t stride) {
     if (begin >= npix) return 0;
     return (npix - begin + stride - 1) / stride;
@@ -271,6 +394,38 @@ int launch(tpt_ctx* c, int mode, int spp, int64_t begin, int64_t stride, int64_t
         else
             hipLaunchKernelGGL(tpt_pt_kernel<false>, dim3((unsigned)qblocks), dim3(kBlock), shmem, c->stream, c->ds,
                                spp, begin, stride, count, dlist, drows, Q);
+    } else if (!c->bdpt_mono) {
+        int rc = ensure_wf(c, count);
+        if (rc) return rc;
+        WfState w = c->wf;
+        w.list = dlist;
+        w.begin = begin;
+        w.stride = stride;
+        w.n = count;
+        w.bounces = c->counters;
+        const unsigned pblocks = (unsigned)((count + kBlock - 1) / kBlock);
+        const float inv = 1.0f / spp;
+        for (int it = 0; it < spp; ++it) {
+            if (lds)
+                hipLaunchKernelGGL(tpt_bdpt_gen_kernel<true>, dim3(pblocks), dim3(kBlock), shmem, c->stream, c->ds, w,
+                                   it == 0 ? 1 : 0);
+            else
+                hipLaunchKernelGGL(tpt_bdpt_gen_kernel<false>, dim3(pblocks), dim3(kBlock), shmem, c->stream, c->ds, w,
+                                   it == 0 ? 1 : 0);
+            size_t bytes = c->scan_bytes;
+            HIP_TRY(c, rocprim::inclusive_scan(c->scan_tmp, bytes, w.np, w.incl, (size_t)count, rocprim::plus<int>(),
+                                               c->stream));
+            hipLaunchKernelGGL(tpt_bdpt_scatter_kernel, dim3(pblocks), dim3(kBlock), 0, c->stream, w);
+            const unsigned cblocks = (unsigned)std::min<int64_t>(8192, (count * 24 + kBlock - 1) / kBlock + 1);
+            if (lds)
+                hipLaunchKernelGGL(tpt_bdpt_conn_kernel<true>, dim3(cblocks), dim3(kBlock), shmem, c->stream, c->ds, w,
+                                   dsplat);
+            else
+                hipLaunchKernelGGL(tpt_bdpt_conn_kernel<false>, dim3(cblocks), dim3(kBlock), shmem, c->stream, c->ds,
+                                   w, dsplat);
+            hipLaunchKernelGGL(tpt_bdpt_fold_kernel, dim3(pblocks), dim3(kBlock), 0, c->stream, w, inv);
+        }
+        hipLaunchKernelGGL(tpt_bdpt_out_kernel, dim3(pblocks), dim3(kBlock), 0, c->stream, w, drows, dlist ? 1 : 0);
     } else {
         if (lds)
             hipLaunchKernelGGL(tpt_bdpt_kernel<true>, dim3((unsigned)blocks), dim3(kBlock), shmem, c->stream, c->ds,
@@ -297,6 +452,19 @@ int launch(tpt_ctx* c, int mode, int spp, int64_t begin, int64_t stride, int64_t
         unsigned long long nb = 0;
         HIP_TRY(c, hipMemcpy(&nb, c->counters, sizeof(nb), hipMemcpyDeviceToHost));
         st->bounces = (int64_t)nb;
+    }
+    if (c->ds.dbg & 8) {  // BDPT phase stamps (TPT_DEBUG_FLAGS & 8)
+        unsigned long long d[8];
+        HIP_TRY(c, hipMemcpy(d, c->counters + 8, sizeof(d), hipMemcpyDeviceToHost));
+        double tot = (double)(d[1] + d[2] + d[3] + d[4]);
+        std::fprintf(stderr, "[tpt dbg] bdpt waves %llu cycles/wave %.4g: camera %.1f%% light %.1f%% rev %.1f%% connect %.1f%%\n",
+                     d[0], tot / d[0], 100.0 * d[1] / tot, 100.0 * d[2] / tot, 100.0 * d[3] / tot, 100.0 * d[4] / tot);
+    }
+    if (c->ds.dbg & 16) {
+        unsigned long long d[8];
+        HIP_TRY(c, hipMemcpy(d, c->counters + 8, sizeof(d), hipMemcpyDeviceToHost));
+        std::fprintf(stderr, "[tpt dbg] bdpt strategies per lane-sample: mean %.2f, wave-max %.2f\n",
+                     (double)d[5] / d[7], (double)d[6] / d[7]);
     }
     if (c->ds.dbg & 2) {  // profiling counters (TPT_DEBUG_FLAGS & 2)
         unsigned long long d[8];
@@ -348,7 +516,8 @@ void tpt_destroy(tpt_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    for (void* p : {(void*)c->blob, (void*)c->rgb, (void*)c->splat, (void*)c->list, (void*)c->rows, (void*)c->counters})
+    for (void* p : {(void*)c->blob, (void*)c->rgb, (void*)c->splat, (void*)c->list, (void*)c->rows, (void*)c->counters,
+                    c->wf_mem, c->scan_tmp})
         if (p) (void)hipFree(p);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -408,6 +577,8 @@ int tpt_upload_scene(tpt_ctx* c, const tpt_scene_desc* d) {
         const char* dbg = std::getenv("TPT_DEBUG_FLAGS");
         ds.dbg = dbg ? std::atoi(dbg) : 0;
         ds.dbgc = c->counters + 8;
+        const char* bk = std::getenv("TPT_BDPT_KERNEL");
+        c->bdpt_mono = bk && bk[0] == 'm';
         const char* q = std::getenv("TPT_PT_LANES");
         c->pt_lanes = q ? std::atoi(q) : 4;  // Q = 4 measured best on one MI355X (Standard, 1024 spp)
         if (c->pt_lanes != 1 && c->pt_lanes != 2 && c->pt_lanes != 4 && c->pt_lanes != 8) c->pt_lanes = 1;

@@ -356,6 +356,72 @@ TPT_D bool shadow_pts_packet(const DScene& s, V3 lc, V3 x, int cull, Packet pk) 
     return shadowed;
 }
 
+// Packet closest hit (BVHAccel::Intersect semantics per lane: same boxes, same
+// leaf order, strict `>` on the f64 distance).  `root` must be wave-uniform; `cull`
+// may differ per lane.  Inactive lanes (active == false) take no part.
+TPT_D Hit traverse_packet(const DScene& s, int root, const Ray& r, int cull, Packet pk, bool active) {
+    Hit best;
+    best.prim = -1;
+    best.dist = 0.0;
+    if (root < 0) return best;
+    int sp = 0;
+    int cur = root;
+    unsigned long long m;
+    {
+        const DNode n = s.nodes[root];
+        m = uni64(__ballot(active && box_hit(n, r)));
+    }
+    for (;;) {
+        if (m != 0) {
+            const DNode n = s.nodes[cur];
+            if (n.a >= 0) {
+                const DNode L = s.nodes[n.a];
+                const DNode R = s.nodes[n.b];
+                const bool mine = (m >> lane_id()) & 1ull;
+                const bool hl = mine && box_hit(L, r);
+                const bool hr = mine && box_hit(R, r);
+                const unsigned long long ml = uni64(__ballot(hl)), mr = uni64(__ballot(hr));
+                if (mr != 0) {
+                    if (ml != 0) {
+                        if (lane_id() == __builtin_ctzll(ml)) { pk.node[sp] = n.a; pk.mask[sp] = ml; }
+                        ++sp;
+                    }
+                    cur = n.b;
+                    m = mr;
+                    continue;
+                }
+                if (ml != 0) { cur = n.a; m = ml; continue; }
+            } else if (n.a != kEmptyLeaf) {
+                if ((m >> lane_id()) & 1ull) {
+                    const int prim = -1 - n.a;
+                    double dist;
+                    bool h;
+                    if (prim < s.ntri) h = tri_test(s.tris[prim], r, cull, dist);
+                    else h = sphere_test(s.sph[prim - s.ntri], r, cull, dist);
+                    if (h && (best.prim < 0 || best.dist > dist)) { best.dist = dist; best.prim = prim; }
+                }
+            }
+        }
+        if (sp == 0) break;
+        --sp;
+        cur = uni(pk.node[sp]);
+        m = uni64(pk.mask[sp]);
+    }
+    return best;
+}
+// Scene::Intersect (Scene.cpp:21-35), packet form.
+TPT_D Hit traverse(const DScene& s, int root, const Ray& r, int cull, int* stk);
+TPT_D PTV scene_intersect_packet(const DScene& s, const Ray& r, int cull, Packet pk, bool active = true) {
+    Hit h = traverse_packet(s, 0, r, cull, pk, active);
+    PTV v = ptv_bg();
+    if (h.prim >= 0) {
+        hit_geometry(s, r, h, v.x, v.N);
+        v.type = T_MID;
+        v.prim = h.prim;
+    }
+    return v;
+}
+
 // ------------------------------------------------------------ materials --
 struct Mat {
     int type;
