@@ -100,6 +100,7 @@ def main():
         torch.cuda.set_device(0)
 
     import pytpt
+    import sharding
     dev = torch.cuda.current_device()
     ctx = pytpt.Context(dev)
     preset = pytpt.Preset(a.scene)
@@ -107,12 +108,11 @@ def main():
     W, H = ctx.width, ctx.height
     fb = torch.zeros(2, H * W * 3, dtype=torch.float32, device="cuda")  # rgb + splat, one reduce buffer
     m = pytpt.MODE_PT if mode == "pt" else pytpt.MODE_BDPT
-    shard_begin, shard_stride = rank, world
+    shard_begin, shard_stride = sharding.shard(rank, world)  # Renderer.cpp:38 interleave
 
     def step():
         st = ctx.render_device(spp, m, fb[0].data_ptr(), fb[1].data_ptr(), shard_begin, shard_stride)
-        if dist is not None:
-            dist.reduce(fb, dst=0)  # framebuffer + splat sum onto rank 0 (RCCL over xGMI)
+        sharding.reduce_frame(dist, fb, dst=0)  # framebuffer + splat sum onto rank 0 (RCCL over xGMI)
         return st
 
     for _ in range(a.warmup):
