@@ -383,6 +383,54 @@ TPT_D void rec_store(const WfState& w, int slot, int64_t k, const BVert& v) {
     r[8 * n] = v.alpha.x; r[9 * n] = v.alpha.y; r[10 * n] = v.alpha.z;
     r[11 * n] = v.q1; r[12 * n] = v.q8;
 }
+TPT_D void rec_store_q(const WfState& w, int slot, int64_t k, float q1, float q8) {
+    float* r = w.rec + (int64_t)slot * kRecF * w.n + k;
+    r[11 * w.n] = q1;
+    r[12 * w.n] = q8;
+}
+
+// fill_path + path_rev streamed into the HBM records (slots base+start+1, ...):
+// the same vertices, draws and float ops, but only a window of three vertices is
+// live.  Vertex j's reverse pdf needs P[j], P[j+1] and P[j+2].x, so it is computed
+// as soon as P[j+2] has been appended -- the private 2 x 16-vertex arrays (1.8 KB
+// of scratch per lane) are gone.  `prev` = P[start-1], `cur` = P[start], both
+// already stored.
+template <bool kPacket>
+TPT_D int fill_path_rec(const DScene& s, const WfState& w, int64_t k, int base, BVert prev, BVert cur, int start,
+                        uint32_t& rs, Packet pk, int* stk) {
+    int count = start + 1;
+    for (int i = start; i < kMaxLen - 1; i++) {
+        if (cur.type == T_BG) break;
+        V3 wo = normalized(prev.x - cur.x);
+        const Mat m = load_mat(s, prim_mat(s, cur.prim));
+        float raw;
+        V3 wi = mat_sample(m, wo, cur.N, &raw, rs);
+        const float rr = i > 4 ? .8f : 1.f;
+        if (rng_float(rs) > rr) break;
+        float ct = (float)dabs_(dot3(cur.N, wi));
+        float sr = safe_div(raw, ct);
+        const Ray nr = make_ray(cur.x, wi);
+        const int cl = dot3(cur.N, wi) > 0.0f ? TPT_CULL_BACK : TPT_CULL_FRONT;
+        PTV it = kPacket ? scene_intersect_packet(s, nr, cl, pk) : scene_intersect(s, nr, cl, stk);
+        float pdf = srpdf_to_area(sr, cur.type, cur.x, cur.N, it.type, it.x, it.N);
+        if (pdf == 0.0f) break;
+        V3 bsdf = eval_bsdf(m, wo, wi, cur.N, false);
+        BVert nx;
+        nx.x = it.x; nx.N = it.N; nx.type = it.type; nx.prim = it.prim;
+        nx.pdf = pdf * rr;
+        nx.alpha = divs(cur.alpha * safe_div(bsdf, sr), rr);
+        nx.q1 = nx.q8 = 0.0f;
+        rec_store(w, base + i + 1, k, nx);
+        count++;
+        // path_rev for j = i - 1: Append(P[j]) after last = P[i], Pre = P[i+1]
+        const float rev = append_pdf(s, cur.type, cur.prim, cur.x, cur.N, nx.x, prev.type, prev.x, prev.N);
+        rec_store_q(w, base + i - 1, k, safe_div(rev * 1.f, prev.pdf), safe_div(rev * .8f, prev.pdf));
+        prev = cur;
+        cur = nx;
+    }
+    return count;
+}
+
 struct GlobPaths {  // one pixel's paths in the HBM records
     const float* rec;
     int64_t n, k;

@@ -59,7 +59,7 @@ TPT_D int* stage_scene(DScene& s) {
 }
 
 #ifndef TPT_PT_MINWAVES
-#define TPT_PT_MINWAVES 3  // waves per SIMD the PT kernel's register budget must allow (3 measured best)
+#define TPT_PT_MINWAVES 4  // waves per SIMD the PT kernel's register budget must allow (4 measured best)
 #endif
 
 // PT (Renderer.cpp:38-52 with PathTrace), replay-exact, Q lanes per pixel.
@@ -110,12 +110,12 @@ __global__ __launch_bounds__(kBlock, TPT_PT_MINWAVES) void tpt_pt_kernel(DScene 
     const bool hit = on && v.type != T_BG;
     V3 acc = v3s(0.0f);
     if (hit) {
-        PTHit h;
-        h.x = v.x;
-        h.n = v.N;
-        h.wo = -dir;
-        h.mat = prim_mat(s, v.prim);
-        const Mat m = load_mat(s, h.mat);
+        const int mi = prim_mat(s, v.prim);
+        const Mat m = load_mat(s, mi);
+        PixPark px;
+        px.base = reinterpret_cast<float*>(tpt_smem + (size_t)s.max_stack * kBlock * sizeof(int) +
+                                           (kLds ? (size_t)s.lds_bytes : 0));
+        px.park(v.x, v.N, -dir, mi, m);
         const float inv = 1.0f / spp;
         uint32_t rs = (uint32_t)((int)i + 1);  // ResetRandom(i + 1), Renderer.cpp:42
         rs = skip_samples(rs, m.type, s.light_draws, q);
@@ -123,7 +123,7 @@ __global__ __launch_bounds__(kBlock, TPT_PT_MINWAVES) void tpt_pt_kernel(DScene 
         for (int j0 = 0; j0 < spp; j0 += Q) {
             V3 L = v3s(0.0f);
             if (j0 + q < spp) {
-                L = mul(pt_sample(s, h, m, rs, stk, pk), inv);
+                L = mul(pt_sample(s, px, rs, stk, pk), inv);
                 if (Q > 1) rs = skip_samples(rs, m.type, s.light_draws, Q - 1);
             }
             if (Q == 1) {
@@ -169,22 +169,53 @@ __global__ __launch_bounds__(kBlock) void tpt_bdpt_kernel(DScene s, int spp, int
 }
 
 // ---- wavefront BDPT kernels (see tpt_bdpt.h, "wavefront") --------------------
+#ifndef TPT_GEN_MINWAVES
+#define TPT_GEN_MINWAVES 4  // waves per SIMD (measured: 4 beats 3 and 5)
+#endif
+#ifndef TPT_CONN_MINWAVES
+#define TPT_CONN_MINWAVES 4  // waves per SIMD (measured: 4 beats 2, 3 and 5)
+#endif
+
 template <bool kLds>
-__global__ __launch_bounds__(kBlock) void tpt_bdpt_gen_kernel(DScene s, WfState w, int first) {
+__global__ __launch_bounds__(kBlock, TPT_GEN_MINWAVES) void tpt_bdpt_gen_kernel(DScene s, WfState w, int first) {
     int* stk = stage_scene<kLds>(s);
     TPT_PACKET_DECL
     const int64_t k = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (k >= w.n) return;
     const int64_t i = wf_pixel(w, k);
-    BVert C[kMaxLen], L[kMaxLen], c0, c1;
+    BVert c0, c1;
     camera_vertices(s, i, c0, c1, stk);
     uint32_t rs = first ? (uint32_t)((int)i + 1) : w.rng[k];  // ResetRandom(i + 1), Renderer.cpp:42
     if (first) { w.acc[3 * k] = 0.0f; w.acc[3 * k + 1] = 0.0f; w.acc[3 * k + 2] = 0.0f; }
-    int cn, ln;
-    generate_paths<false>(s, c0, c1, rs, C, L, cn, ln, pk, stk);
+    // generate_paths (tpt_bdpt.h) with the vertices streamed into the records
+    rec_store(w, 0, k, c0);
+    rec_store(w, 1, k, c1);
+    const int cn = fill_path_rec<false>(s, w, k, 0, c0, c1, 1, rs, pk, stk);
+    // GenerateLightPath (BDPT.cpp:61-90) from m_emissionObjects[0]
+    const DObj lo = s.objs[s.emitters[0]];
+    V3 pc, pn;
+    int pp;
+    object_sample(s, lo, pc, pn, pp, rs);
+    BVert l0;
+    l0.x = pc; l0.N = pn; l0.type = T_LIGHT; l0.prim = pp;
+    l0.pdf = lo.pdf;
+    l0.alpha = divs(load_mat(s, lo.mat).em, l0.pdf);
+    l0.q1 = l0.q8 = 0.0f;
+    float pdf1;
+    V3 wi = cosine_sample(pn, pdf1, rs);
+    float ct = (float)dot3(l0.N, wi);
+    pdf1 = safe_div(pdf1, ct);
+    PTV it = scene_intersect(s, make_ray(l0.x, wi), TPT_CULL_BACK, stk);
+    BVert l1;
+    l1.x = it.x; l1.N = it.N; l1.type = it.type; l1.prim = it.prim;
+    l1.pdf = srpdf_to_area(pdf1, T_LIGHT, l0.x, l0.N, it.type, it.x, it.N);
+    l1.alpha = v3s(0.0f);  // fresh InternalPathVertex (BDPT.hpp:19)
+    l1.q1 = l1.q8 = 0.0f;
+    if (pdf1 != 0.0f) l1.alpha = safe_div(l0.alpha, pdf1);
+    rec_store(w, kMaxLen, k, l0);
+    rec_store(w, kMaxLen + 1, k, l1);
+    const int ln = (pdf1 == 0.0f && it.type == T_BG) ? 2 : fill_path_rec<false>(s, w, k, kMaxLen, l0, l1, 1, rs, pk, stk);
     w.rng[k] = rs;
-    for (int j = 0; j < cn; ++j) rec_store(w, j, k, C[j]);
-    for (int j = 0; j < ln; ++j) rec_store(w, kMaxLen + j, k, L[j]);
     w.cnt[k] = cn | (ln << 16);
     w.np[k] = cn * (ln + 1) - 1;
     atomicAdd(w.bounces, (unsigned long long)(cn + ln));
@@ -198,7 +229,7 @@ __global__ __launch_bounds__(kBlock) void tpt_bdpt_scatter_kernel(WfState w) {
 }
 
 template <bool kLds>
-__global__ __launch_bounds__(kBlock) void tpt_bdpt_conn_kernel(DScene s, WfState w, float* __restrict__ splat) {
+__global__ __launch_bounds__(kBlock, TPT_CONN_MINWAVES) void tpt_bdpt_conn_kernel(DScene s, WfState w, float* __restrict__ splat) {
     int* stk = stage_scene<kLds>(s);
     TPT_PACKET_DECL
     const int64_t total = w.incl[w.n - 1];
@@ -289,7 +320,7 @@ struct tpt_ctx {
     float* rows = nullptr;
     int64_t rows_cap = 0;
     unsigned long long* counters = nullptr;
-    int pt_lanes = 4;  // Q: lanes per pixel of the PT kernel (1, 2, 4, 8)
+    int pt_lanes = 8;  // Q: lanes per pixel of the PT kernel (1, 2, 4, 8, 16)
     // wavefront BDPT state (sized for wf_cap pixels)
     void* wf_mem = nullptr;
     int64_t wf_cap = 0;
@@ -388,11 +419,12 @@ int launch(tpt_ctx* c, int mode, int spp, int64_t begin, int64_t stride, int64_t
     if (mode == TPT_MODE_PT) {
         const int Q = c->pt_lanes;
         const int64_t qblocks = (count * Q + kBlock - 1) / kBlock;
+        const size_t pshmem = shmem + (size_t)kPixSlots * kBlock * sizeof(float);
         if (lds)
-            hipLaunchKernelGGL(tpt_pt_kernel<true>, dim3((unsigned)qblocks), dim3(kBlock), shmem, c->stream, c->ds,
+            hipLaunchKernelGGL(tpt_pt_kernel<true>, dim3((unsigned)qblocks), dim3(kBlock), pshmem, c->stream, c->ds,
                                spp, begin, stride, count, dlist, drows, Q);
         else
-            hipLaunchKernelGGL(tpt_pt_kernel<false>, dim3((unsigned)qblocks), dim3(kBlock), shmem, c->stream, c->ds,
+            hipLaunchKernelGGL(tpt_pt_kernel<false>, dim3((unsigned)qblocks), dim3(kBlock), pshmem, c->stream, c->ds,
                                spp, begin, stride, count, dlist, drows, Q);
     } else if (!c->bdpt_mono) {
         int rc = ensure_wf(c, count);
@@ -580,8 +612,8 @@ int tpt_upload_scene(tpt_ctx* c, const tpt_scene_desc* d) {
         const char* bk = std::getenv("TPT_BDPT_KERNEL");
         c->bdpt_mono = bk && bk[0] == 'm';
         const char* q = std::getenv("TPT_PT_LANES");
-        c->pt_lanes = q ? std::atoi(q) : 4;  // Q = 4 measured best on one MI355X (Standard, 1024 spp)
-        if (c->pt_lanes != 1 && c->pt_lanes != 2 && c->pt_lanes != 4 && c->pt_lanes != 8) c->pt_lanes = 1;
+        c->pt_lanes = q ? std::atoi(q) : 8;  // Q = 8 measured best on one MI355X (Standard, 1024 spp)
+        if (c->pt_lanes != 1 && c->pt_lanes != 2 && c->pt_lanes != 4 && c->pt_lanes != 8 && c->pt_lanes != 16) c->pt_lanes = 1;
     }
     c->ds = ds;
     c->hs = std::move(hs);

@@ -772,59 +772,125 @@ TPT_D Hit object_hit(const DScene& s, const DObj& o, const Ray& r, int cull, int
 }
 
 // ------------------------------------------------------------------- PT ---
+// The camera hit and its material are invariant over a pixel's spp loop.  Held in
+// registers across the loop they cost ~25 VGPRs at every point of the sample body
+// and push the kernel into scratch spills; instead each lane parks them in LDS
+// ([slot][kBlock] floats, conflict-free) and re-reads them where they are used.  The
+// empty asm makes the lane offset opaque, so the compiler can neither hoist the
+// reads out of the loop nor keep one read alive across the sample body.
+enum PixSlot {
+    kPxMat = 0,
+    kPxType,
+    kPxIorD,
+    kPxRough,
+    kPxX,
+    kPxN = kPxX + 3,
+    kPxWo = kPxN + 3,
+    kPxKd = kPxWo + 3,
+    kPxIorM = kPxKd + 3,
+    kPxIorMK = kPxIorM + 3,
+    kPixSlots = kPxIorMK + 3
+};
+struct PixPark {
+    float* base;  // kPixSlots x kBlock floats of LDS
+    TPT_D const float* lane() const {
+        unsigned off = threadIdx.x;
+        asm volatile("" : "+v"(off));
+        return base + off;
+    }
+    TPT_D V3 v(int k) const {
+        const float* p = lane();
+        return v3(p[k * kBlock], p[(k + 1) * kBlock], p[(k + 2) * kBlock]);
+    }
+    TPT_D int mat_index() const { return __float_as_int(lane()[kPxMat * kBlock]); }
+    TPT_D Mat mat() const {
+        const float* p = lane();
+        Mat m;
+        m.type = __float_as_int(p[kPxType * kBlock]);
+        m.ior_d = p[kPxIorD * kBlock];
+        m.rough = p[kPxRough * kBlock];
+        m.kd = v3(p[kPxKd * kBlock], p[(kPxKd + 1) * kBlock], p[(kPxKd + 2) * kBlock]);
+        m.ior_m = v3(p[kPxIorM * kBlock], p[(kPxIorM + 1) * kBlock], p[(kPxIorM + 2) * kBlock]);
+        m.ior_m_k = v3(p[kPxIorMK * kBlock], p[(kPxIorMK + 1) * kBlock], p[(kPxIorMK + 2) * kBlock]);
+        m.em = v3s(0.0f);  // emission is read from the scene where it is used
+        return m;
+    }
+    TPT_D void put(int k, float x) { base[k * kBlock + threadIdx.x] = x; }
+    TPT_D void put3(int k, V3 a) {
+        put(k, a.x);
+        put(k + 1, a.y);
+        put(k + 2, a.z);
+    }
+    TPT_D void park(V3 x, V3 n, V3 wo, int mi, const Mat& m) {
+        put(kPxMat, __int_as_float(mi));
+        put(kPxType, __int_as_float(m.type));
+        put(kPxIorD, m.ior_d);
+        put(kPxRough, m.rough);
+        put3(kPxX, x);
+        put3(kPxN, n);
+        put3(kPxWo, wo);
+        put3(kPxKd, m.kd);
+        put3(kPxIorM, m.ior_m);
+        put3(kPxIorMK, m.ior_m_k);
+    }
+};
+
 // PathTrace at HEAD (PathTracer.cpp:44-134): emission of the camera hit + MIS
 // direct lighting from every emitter, then the unconditional `break` (:109).
 // The camera hit is the same for every sample of a pixel (no jitter,
-// SceneRenderingHelper.cpp:16-22) and is hoisted out of the spp loop by the caller.
-struct PTHit {
-    V3 x, n, wo;
-    int mat;
-};
-TPT_D V3 pt_sample(const DScene& s, const PTHit& h, const Mat& m, uint32_t& rs, int* stk, Packet pk) {
+// SceneRenderingHelper.cpp:16-22): the caller computes it once and parks it in `px`.
+TPT_D V3 pt_sample(const DScene& s, PixPark px, uint32_t& rs, int* stk, Packet pk) {
     V3 result = v3s(0.0f);
-    if (s.mats[h.mat].has_em) result = result + m.em;
+    {
+        const DMat& dm = s.mats[px.mat_index()];
+        if (dm.has_em) result = result + v3(dm.em[0], dm.em[1], dm.em[2]);
+    }
     float pdf_b;
-    V3 wib = mat_sample(m, h.wo, h.n, &pdf_b, rs);
+    V3 wib = mat_sample(px.mat(), px.v(kPxWo), px.v(kPxN), &pdf_b, rs);
     for (int li = 0; li < s.n_emitters; ++li) {
         const DObj o = s.objs[s.emitters[li]];
         // DirectLightSampler::sample (PathTracer.cpp:26-40)
         V3 pc, pn;
         int pp;
         object_sample(s, o, pc, pn, pp, rs);
-        V3 wil = pc - h.x;
+        V3 wil = pc - px.v(kPxX);
         float d2 = (float)dot3(wil, wil);
         wil = normalized(wil);
         float ct = (float)dot3(pn, -wil);
         float pll = (float)((double)o.pdf * d2 / (double)fabs_(ct));
-        float plb = mat_pdf(m, h.wo, h.n, wil);
-        // DirectLightSampler::pdf (PathTracer.cpp:14-24) on the BSDF direction
-        Ray rb = make_ray(h.x, wib);
-        Hit hnc, hb;
-        object_hit_nocull_back(s, o, rb, hnc, hb, stk);
-        float pbl = 0.0f;
-        if (hnc.prim >= 0) {
-            V3 hx, hn;
-            hit_geometry(s, rb, hnc, hx, hn);
-            float ld2 = (float)dot3(hx - h.x, hx - h.x);
-            float c = (float)dot3(hn, -wib);
-            if (c != 0.0f) pbl = (float)((double)o.pdf * ld2 / (double)fabs_(c));
-        }
         V3 ev = v3s(0.0f);
-        if (pdf_b + pbl > 0.0f) {
-            if (hb.prim >= 0) {
+        {
+            // DirectLightSampler::pdf (PathTracer.cpp:14-24) on the BSDF direction
+            const V3 hx0 = px.v(kPxX);
+            Ray rb = make_ray(hx0, wib);
+            Hit hnc, hb;
+            object_hit_nocull_back(s, o, rb, hnc, hb, stk);
+            float pbl = 0.0f;
+            if (hnc.prim >= 0) {
                 V3 hx, hn;
-                hit_geometry(s, rb, hb, hx, hn);
-                if (!shadow_pts_packet(s, hx, h.x, TPT_CULL_BACK, pk))
-                    ev = ev + divs(eval_bsdf(m, h.wo, wib, h.n, true), 1e-4f + pdf_b + pbl);
+                hit_geometry(s, rb, hnc, hx, hn);
+                float ld2 = (float)dot3(hx - hx0, hx - hx0);
+                float c = (float)dot3(hn, -wib);
+                if (c != 0.0f) pbl = (float)((double)o.pdf * ld2 / (double)fabs_(c));
+            }
+            if (pdf_b + pbl > 0.0f) {
+                if (hb.prim >= 0) {
+                    V3 hx, hn;
+                    hit_geometry(s, rb, hb, hx, hn);
+                    if (!shadow_pts_packet(s, hx, px.v(kPxX), TPT_CULL_BACK, pk))
+                        ev = ev + divs(eval_bsdf(px.mat(), px.v(kPxWo), wib, px.v(kPxN), true), 1e-4f + pdf_b + pbl);
+                }
             }
         }
+        // the light branch (PathTracer.cpp:95-106); plb is pure, so it is computed here
+        float plb = mat_pdf(px.mat(), px.v(kPxWo), px.v(kPxN), wil);
         if (pll + plb > 0.0f) {
-            Ray rl = make_ray(h.x, wil);
+            Ray rl = make_ray(px.v(kPxX), wil);
             Hit hl = object_hit(s, o, rl, TPT_CULL_BACK, stk);
             V3 hx = v3s(0.0f), hn;  // default Intersection::coords when missed (Intersection.hpp:14-21)
             if (hl.prim >= 0) hit_geometry(s, rl, hl, hx, hn);
-            if (!shadow_pts_packet(s, hx, h.x, TPT_CULL_BACK, pk))
-                ev = ev + divs(eval_bsdf(m, h.wo, wil, h.n, true), 1e-4f + pll + plb);
+            if (!shadow_pts_packet(s, hx, px.v(kPxX), TPT_CULL_BACK, pk))
+                ev = ev + divs(eval_bsdf(px.mat(), px.v(kPxWo), wil, px.v(kPxN), true), 1e-4f + pll + plb);
         }
         result = result + ev * load_mat(s, o.mat).em;
     }
