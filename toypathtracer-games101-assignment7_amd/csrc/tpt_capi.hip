@@ -540,6 +540,14 @@ int tpt_create(int device, tpt_ctx** out) {
         delete c;
         return TPT_E_DEVICE;
     }
+    // Fail here, not in the first launch, when this device has no code object of
+    // ours (the library is built for gfx950 only; there is no fallback).
+    hipFuncAttributes fa;
+    if (hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(tpt_scale_kernel)) != hipSuccess) {
+        (void)hipGetLastError();
+        tpt_destroy(c);
+        return TPT_E_DEVICE;
+    }
     *out = c;
     return TPT_OK;
 }
