@@ -14,7 +14,8 @@ Roofline: the hot kernel's ALGORITHMIC scene-fetch bytes (BVH no
 popped x 32 B + triangle tests x 48 B, counted on the reference traversal; 2,073 B
 per Standard PT sample) / its average device time (HIP events inside libtpt on the
 stream the kernel runs on) against 8 TB/s.  The scene is L2-resident, so this is a
-modelled yardstick; `traffic` is the measured HBM bytes when a PMC run is supplied.
+modelled yardstick; `traffic` is the memory-side bytes per launch measured by
+rocprofv3 FETCH_SIZE/WRITE_SIZE passes (profiles/traffic.json, scripts/pmc_traffic.py).
 
 cpu_baseline: the REAL reference renderer (oracle/_ref/libref.so, Renderer::Render
 with std::async threads) on a bounded sample, rank 0 only; falls back to the CPU
@@ -48,8 +49,18 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-threads", type=int, default=None)
     ap.add_argument("--traffic-bytes", type=float, default=None,
-                    help="HBM bytes per launch from a rocprofv3 --pmc run (profiles/)")
+                    help="HBM bytes per launch (default: profiles/traffic.json, made by scripts/pmc_traffic.py)")
     return ap.parse_args()
+
+
+def pmc_traffic(scene, mode):
+    """Per-launch memory-side bytes of the dominant kernel, measured by rocprofv3
+    FETCH_SIZE / WRITE_SIZE passes of this build (profiles/traffic.json)."""
+    path = os.path.join(ROOT, "profiles", "traffic.json")
+    if not os.path.exists(path):
+        return None
+    e = json.load(open(path)).get("%s/%s" % (scene, mode))
+    return float(e["bytes_per_launch"]) if e else None
 
 
 def cpu_baseline(mode, scene, threads):
@@ -144,8 +155,8 @@ def main():
         achieved = (shard_samples * b_alg / (kernel_ms / 1e3) / 1e9) if b_alg else None
         roofline = {"bound": "hbm", "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
-                    "traffic": a.traffic_bytes,
-                    "kernel": "tpt_%s_kernel" % mode, "kernel_ms": round(kernel_ms, 3),
+                    "traffic": a.traffic_bytes if a.traffic_bytes is not None else pmc_traffic(a.scene, mode),
+                    "kernel": "tpt_pt_kernel" if mode == "pt" else "bdpt wavefront sequence (gen+scan+scatter+conn+fold) x spp", "kernel_ms": round(kernel_ms, 3),
                     "bytes_per_sample_alg": b_alg, "samples_per_launch": shard_samples,
                     "note": "algorithmic scene-fetch bytes (SURVEY 8d); scene is L2-resident, real bound is VALU"}
         cpu = None
