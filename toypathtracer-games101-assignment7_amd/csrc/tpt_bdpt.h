@@ -351,19 +351,21 @@ TPT_D void bdpt_pixel(const DScene& s, int64_t i, int spp, V3& acc, float* splat
 //   gen:     generate both subpaths (RNG-sequential per pixel) and write them to
 //            HBM as SoA records [path*16+vertex][field][pixel];
 //   scan:    inclusive prefix sum of the strategy counts cn*(ln+1)-1;
-//   scatter: owner[g] = pixel for every strategy g;
+//   scatter: task[g] = (pixel, t, s) for every strategy g;
 //   connect: ONE LANE PER STRATEGY (PathWeight), so a wave's work is 64 strategies
 //            instead of the longest lane's cn*(ln+1) (measured 18 mean vs 73 max);
 //            t = 1 splats go straight to the splat buffer;
 //   fold:    per pixel, result += w over its strategies in (t, s) order (t > 1) and
 //            fb += (1/spp) * result -- the reference's summation order.
-constexpr int kRecF = 13;  // x(3) N(3) type|prim pdf alpha(3) q1 q8
+// One vertex record = 64 B = four float4: (x, type|prim) (N, pdf) (alpha, -) (q1, q8, -, -),
+// laid out [pixel][slot] so a vertex is one contiguous line segment (4 x 16-B accesses).
+constexpr int kRecV = 4;  // float4 per vertex record
 struct WfState {
-    float* rec;           // 32 * kRecF * n floats
+    float4* rec;          // n * 32 * kRecV float4
     int* cnt;             // cn | ln << 16
     int* np;              // strategies per pixel
     int* incl;            // inclusive scan of np
-    int* owner;           // strategy -> pixel
+    unsigned long long* task;  // strategy -> pixel | t << 40 | s << 48
     float* res;           // 3 floats per strategy
     uint32_t* rng;        // XorShift state per pixel stream
     float* acc;           // 3 floats per pixel
@@ -373,20 +375,16 @@ struct WfState {
 };
 TPT_D int64_t wf_pixel(const WfState& w, int64_t k) { return w.list ? w.list[k] : w.begin + k * w.stride; }
 TPT_D int tp_pack(int type, int prim) { return (prim + 1) * 4 + type; }
+TPT_D float4* rec_at(float4* rec, int64_t k, int slot) { return rec + ((k * (2 * kMaxLen) + slot) * kRecV); }
 TPT_D void rec_store(const WfState& w, int slot, int64_t k, const BVert& v) {
-    float* r = w.rec + (int64_t)slot * kRecF * w.n + k;
-    const int64_t n = w.n;
-    r[0 * n] = v.x.x; r[1 * n] = v.x.y; r[2 * n] = v.x.z;
-    r[3 * n] = v.N.x; r[4 * n] = v.N.y; r[5 * n] = v.N.z;
-    r[6 * n] = __builtin_bit_cast(float, tp_pack(v.type, v.prim));
-    r[7 * n] = v.pdf;
-    r[8 * n] = v.alpha.x; r[9 * n] = v.alpha.y; r[10 * n] = v.alpha.z;
-    r[11 * n] = v.q1; r[12 * n] = v.q8;
+    float4* r = rec_at(w.rec, k, slot);
+    r[0] = make_float4(v.x.x, v.x.y, v.x.z, __builtin_bit_cast(float, tp_pack(v.type, v.prim)));
+    r[1] = make_float4(v.N.x, v.N.y, v.N.z, v.pdf);
+    r[2] = make_float4(v.alpha.x, v.alpha.y, v.alpha.z, 0.0f);
+    r[3] = make_float4(v.q1, v.q8, 0.0f, 0.0f);
 }
 TPT_D void rec_store_q(const WfState& w, int slot, int64_t k, float q1, float q8) {
-    float* r = w.rec + (int64_t)slot * kRecF * w.n + k;
-    r[11 * w.n] = q1;
-    r[12 * w.n] = q8;
+    *reinterpret_cast<float2*>(rec_at(w.rec, k, slot) + 3) = make_float2(q1, q8);
 }
 
 // fill_path + path_rev streamed into the HBM records (slots base+start+1, ...):
@@ -432,23 +430,27 @@ TPT_D int fill_path_rec(const DScene& s, const WfState& w, int64_t k, int base, 
 }
 
 struct GlobPaths {  // one pixel's paths in the HBM records
-    const float* rec;
-    int64_t n, k;
+    const float4* rec;  // this pixel's 32 vertex records
     TPT_D BVert load(int slot) const {
-        const float* r = rec + (int64_t)slot * kRecF * n + k;
+        const float4* r = rec + slot * kRecV;
+        const float4 a = r[0], b = r[1], c = r[2];
+        const float2 q = *reinterpret_cast<const float2*>(r + 3);
         BVert v;
-        v.x = v3(r[0 * n], r[1 * n], r[2 * n]);
-        v.N = v3(r[3 * n], r[4 * n], r[5 * n]);
-        const int tp = __builtin_bit_cast(int, r[6 * n]);
+        v.x = v3(a.x, a.y, a.z);
+        const int tp = __builtin_bit_cast(int, a.w);
         v.type = tp & 3;
         v.prim = (tp >> 2) - 1;
-        v.pdf = r[7 * n];
-        v.alpha = v3(r[8 * n], r[9 * n], r[10 * n]);
-        v.q1 = r[11 * n];
-        v.q8 = r[12 * n];
+        v.N = v3(b.x, b.y, b.z);
+        v.pdf = b.w;
+        v.alpha = v3(c.x, c.y, c.z);
+        v.q1 = q.x;
+        v.q8 = q.y;
         return v;
     }
-    TPT_D float q(int slot, bool r8) const { return rec[((int64_t)slot * kRecF + (r8 ? 12 : 11)) * n + k]; }
+    TPT_D float q(int slot, bool r8) const {
+        const float* r = reinterpret_cast<const float*>(rec + slot * kRecV + 3);
+        return r8 ? r[1] : r[0];
+    }
     TPT_D BVert cam(int j) const { return load(j); }
     TPT_D BVert lit(int j) const { return load(kMaxLen + j); }
     TPT_D float camq(int j, bool r8) const { return q(j, r8); }

@@ -225,7 +225,12 @@ __global__ __launch_bounds__(kBlock) void tpt_bdpt_scatter_kernel(WfState w) {
     const int64_t k = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (k >= w.n) return;
     const int e = w.incl[k], b = e - w.np[k];
-    for (int g = b; g < e; ++g) w.owner[g] = (int)k;
+    const int ln = w.cnt[k] >> 16;
+    for (int g = b; g < e; ++g) {
+        const int pi = g - b + 1;  // strategy index in (t, s) order; pi = 0 skipped
+        const unsigned long long t = (unsigned long long)(pi / (ln + 1) + 1), sl = (unsigned long long)(pi % (ln + 1));
+        w.task[g] = (unsigned long long)k | (t << 40) | (sl << 48);
+    }
 }
 
 template <bool kLds>
@@ -235,15 +240,11 @@ __global__ __launch_bounds__(kBlock, TPT_CONN_MINWAVES) void tpt_bdpt_conn_kerne
     const int64_t total = w.incl[w.n - 1];
     const V3 eye = v3(s.eye[0], s.eye[1], s.eye[2]);
     for (int64_t g = (int64_t)blockIdx.x * kBlock + threadIdx.x; g < total; g += (int64_t)gridDim.x * kBlock) {
-        const int k = w.owner[g];
-        const int b = w.incl[k] - w.np[k];
-        const int pi = (int)(g - b) + 1;  // strategy index in (t, s) order; pi = 0 skipped
-        const int ln = w.cnt[k] >> 16;
-        const int t = pi / (ln + 1) + 1, sl = pi % (ln + 1);
+        const unsigned long long tk = w.task[g];
+        const int64_t k = (int64_t)(tk & 0xffffffffffull);
+        const int t = (int)((tk >> 40) & 0xff), sl = (int)(tk >> 48);
         GlobPaths P;
-        P.rec = w.rec;
-        P.n = w.n;
-        P.k = k;
+        P.rec = rec_at(w.rec, k, 0);
         const V3 v = vmax0(path_weight<GlobPaths, false>(s, P, sl, t, pk, stk));
         if (t > 1) {
             w.res[3 * g] = v.x;
@@ -380,18 +381,18 @@ int ensure_wf(tpt_ctx* c, int64_t n) {
     c->wf_cap = 0;
     const int64_t maxs = (int64_t)kMaxLen * (kMaxLen + 1) - 1;
     auto al = [](int64_t b) { return (b + 255) & ~(int64_t)255; };
-    const int64_t b_rec = al(2 * kMaxLen * kRecF * n * 4), b_i = al(n * 4), b_own = al(n * maxs * 4),
+    const int64_t b_rec = al(2 * kMaxLen * kRecV * n * 16), b_i = al(n * 4), b_own = al(n * maxs * 8),
                   b_res = al(n * maxs * 12), b_acc = al(n * 12);
     const int64_t total = b_rec + 4 * b_i + b_own + b_res + b_acc;
     HIP_TRY(c, hipMalloc(&c->wf_mem, total));
     char* p = (char*)c->wf_mem;
     WfState& w = c->wf;
-    w.rec = (float*)p; p += b_rec;
+    w.rec = (float4*)p; p += b_rec;
     w.cnt = (int*)p; p += b_i;
     w.np = (int*)p; p += b_i;
     w.incl = (int*)p; p += b_i;
     w.rng = (uint32_t*)p; p += b_i;
-    w.owner = (int*)p; p += b_own;
+    w.task = (unsigned long long*)p; p += b_own;
     w.res = (float*)p; p += b_res;
     w.acc = (float*)p;
     size_t bytes = 0;
