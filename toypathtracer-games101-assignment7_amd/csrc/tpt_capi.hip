@@ -325,7 +325,9 @@ struct tpt_ctx {
     // wavefront BDPT state (sized for wf_cap pixels)
     void* wf_mem = nullptr;
     int64_t wf_cap = 0;
-    WfState wf{};
+    WfState wf[2]{};                  // double-buffered: gen(it+1) overlaps connect(it)
+    hipStream_t stream2 = nullptr;    // connect + fold
+    hipEvent_t ev_gen[2]{}, ev_fold[2]{};
     void* scan_tmp = nullptr;
     size_t scan_bytes = 0;
     bool bdpt_mono = false;  // TPT_BDPT_KERNEL=mono: one lane per pixel stream (A/B only)
@@ -383,18 +385,22 @@ int ensure_wf(tpt_ctx* c, int64_t n) {
     auto al = [](int64_t b) { return (b + 255) & ~(int64_t)255; };
     const int64_t b_rec = al(2 * kMaxLen * kRecV * n * 16), b_i = al(n * 4), b_own = al(n * maxs * 8),
                   b_res = al(n * maxs * 12), b_acc = al(n * 12);
-    const int64_t total = b_rec + 4 * b_i + b_own + b_res + b_acc;
+    const int64_t per_buf = b_rec + 3 * b_i + b_own + b_res;
+    const int64_t total = 2 * per_buf + b_i + b_acc;
     HIP_TRY(c, hipMalloc(&c->wf_mem, total));
     char* p = (char*)c->wf_mem;
-    WfState& w = c->wf;
-    w.rec = (float4*)p; p += b_rec;
-    w.cnt = (int*)p; p += b_i;
-    w.np = (int*)p; p += b_i;
-    w.incl = (int*)p; p += b_i;
-    w.rng = (uint32_t*)p; p += b_i;
-    w.task = (unsigned long long*)p; p += b_own;
-    w.res = (float*)p; p += b_res;
-    w.acc = (float*)p;
+    for (int b = 0; b < 2; ++b) {
+        WfState& w = c->wf[b];
+        w.rec = (float4*)p; p += b_rec;
+        w.cnt = (int*)p; p += b_i;
+        w.np = (int*)p; p += b_i;
+        w.incl = (int*)p; p += b_i;
+        w.task = (unsigned long long*)p; p += b_own;
+        w.res = (float*)p; p += b_res;
+    }
+    c->wf[0].rng = c->wf[1].rng = (uint32_t*)p; p += b_i;
+    c->wf[0].acc = c->wf[1].acc = (float*)p;
+    const WfState& w = c->wf[0];
     size_t bytes = 0;
     HIP_TRY(c, rocprim::inclusive_scan(nullptr, bytes, w.np, w.incl, (size_t)n, rocprim::plus<int>(), c->stream));
     HIP_TRY(c, hipMalloc(&c->scan_tmp, bytes));
@@ -430,15 +436,25 @@ int launch(tpt_ctx* c, int mode, int spp, int64_t begin, int64_t stride, int64_t
     } else if (!c->bdpt_mono) {
         int rc = ensure_wf(c, count);
         if (rc) return rc;
-        WfState w = c->wf;
-        w.list = dlist;
-        w.begin = begin;
-        w.stride = stride;
-        w.n = count;
-        w.bounces = c->counters;
+        // Two streams: gen/scan/scatter of iteration it on c->stream, connect/fold on
+        // c->stream2, with the wavefront state double-buffered so gen(it+1) runs
+        // beside connect(it) and fills the tail of each.  Ordering per pixel is kept:
+        // gen is sequential on one stream (RNG state), fold is sequential on the other
+        // (acc, splat), and buffer b is rewritten by gen(it+2) only after fold(it).
+        HIP_TRY(c, hipEventRecord(c->ev_fold[0], c->stream));
+        HIP_TRY(c, hipStreamWaitEvent(c->stream2, c->ev_fold[0], 0));  // stream2 starts after ev0
         const unsigned pblocks = (unsigned)((count + kBlock - 1) / kBlock);
+        const unsigned cblocks = (unsigned)std::min<int64_t>(8192, (count * 24 + kBlock - 1) / kBlock + 1);
         const float inv = 1.0f / spp;
         for (int it = 0; it < spp; ++it) {
+            const int b = it & 1;
+            WfState w = c->wf[b];
+            w.list = dlist;
+            w.begin = begin;
+            w.stride = stride;
+            w.n = count;
+            w.bounces = c->counters;
+            if (it >= 2) HIP_TRY(c, hipStreamWaitEvent(c->stream, c->ev_fold[b], 0));
             if (lds)
                 hipLaunchKernelGGL(tpt_bdpt_gen_kernel<true>, dim3(pblocks), dim3(kBlock), shmem, c->stream, c->ds, w,
                                    it == 0 ? 1 : 0);
@@ -449,15 +465,23 @@ int launch(tpt_ctx* c, int mode, int spp, int64_t begin, int64_t stride, int64_t
             HIP_TRY(c, rocprim::inclusive_scan(c->scan_tmp, bytes, w.np, w.incl, (size_t)count, rocprim::plus<int>(),
                                                c->stream));
             hipLaunchKernelGGL(tpt_bdpt_scatter_kernel, dim3(pblocks), dim3(kBlock), 0, c->stream, w);
-            const unsigned cblocks = (unsigned)std::min<int64_t>(8192, (count * 24 + kBlock - 1) / kBlock + 1);
+            HIP_TRY(c, hipEventRecord(c->ev_gen[b], c->stream));
+            HIP_TRY(c, hipStreamWaitEvent(c->stream2, c->ev_gen[b], 0));
             if (lds)
-                hipLaunchKernelGGL(tpt_bdpt_conn_kernel<true>, dim3(cblocks), dim3(kBlock), shmem, c->stream, c->ds, w,
+                hipLaunchKernelGGL(tpt_bdpt_conn_kernel<true>, dim3(cblocks), dim3(kBlock), shmem, c->stream2, c->ds, w,
                                    dsplat);
             else
-                hipLaunchKernelGGL(tpt_bdpt_conn_kernel<false>, dim3(cblocks), dim3(kBlock), shmem, c->stream, c->ds,
+                hipLaunchKernelGGL(tpt_bdpt_conn_kernel<false>, dim3(cblocks), dim3(kBlock), shmem, c->stream2, c->ds,
                                    w, dsplat);
-            hipLaunchKernelGGL(tpt_bdpt_fold_kernel, dim3(pblocks), dim3(kBlock), 0, c->stream, w, inv);
+            hipLaunchKernelGGL(tpt_bdpt_fold_kernel, dim3(pblocks), dim3(kBlock), 0, c->stream2, w, inv);
+            HIP_TRY(c, hipEventRecord(c->ev_fold[b], c->stream2));
         }
+        HIP_TRY(c, hipStreamWaitEvent(c->stream, c->ev_fold[(spp - 1) & 1], 0));
+        WfState w = c->wf[0];
+        w.list = dlist;
+        w.begin = begin;
+        w.stride = stride;
+        w.n = count;
         hipLaunchKernelGGL(tpt_bdpt_out_kernel, dim3(pblocks), dim3(kBlock), 0, c->stream, w, drows, dlist ? 1 : 0);
     } else {
         if (lds)
@@ -537,6 +561,11 @@ int tpt_create(int device, tpt_ctx** out) {
     }
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_gen[0], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_gen[1], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_fold[0], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_fold[1], hipEventDisableTiming) != hipSuccess ||
         hipMalloc(&c->counters, sizeof(unsigned long long) * 16) != hipSuccess) {
         delete c;
         return TPT_E_DEVICE;
@@ -560,6 +589,10 @@ void tpt_destroy(tpt_ctx* c) {
     for (void* p : {(void*)c->blob, (void*)c->rgb, (void*)c->splat, (void*)c->list, (void*)c->rows, (void*)c->counters,
                     c->wf_mem, c->scan_tmp})
         if (p) (void)hipFree(p);
+    if (c->stream2) (void)hipStreamSynchronize(c->stream2);
+    for (hipEvent_t e : {c->ev_gen[0], c->ev_gen[1], c->ev_fold[0], c->ev_fold[1]})
+        if (e) (void)hipEventDestroy(e);
+    if (c->stream2) (void)hipStreamDestroy(c->stream2);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->stream) (void)hipStreamDestroy(c->stream);
