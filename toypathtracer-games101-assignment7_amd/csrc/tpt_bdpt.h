@@ -104,7 +104,14 @@ TPT_D bool shadow_v(const DScene& s, const BVert& v1, const BVert& v2, Packet pk
         test = false;  // Scene.cpp:75-78
     }
     bool sh = false;
-    if (test) sh = kPacket ? shadow_pts_packet(s, v1.x, v2.x, cull, pk) : shadow_pts(s, v1.x, v2.x, cull, stk);
+#ifndef TPT_LANE_SHADOW
+#define TPT_LANE_SHADOW 0  // per-lane shadow walk: 0 binary tree, 1 4-wide tree, 2 wave packet on the 4-wide tree
+#endif
+    if (test) {
+        if (kPacket || TPT_LANE_SHADOW == 2) sh = shadow_q_packet(s, v1.x, v2.x, cull, pk);
+        else if (TPT_LANE_SHADOW == 1) sh = shadow_q(s, v1.x, v2.x, cull, stk);
+        else sh = shadow_pts(s, v1.x, v2.x, cull, stk);
+    }
     return sh;
 }
 

@@ -35,7 +35,7 @@ extern __shared__ __align__(16) unsigned char tpt_smem[];
     pk.node = pk_node[threadIdx.x / 64];                                  \
     pk.mask = pk_mask[threadIdx.x / 64];
 
-// Workgroup prologue: LDS = [traversal stack: max_stack x kBlock ints][nodes][tris].
+// Workgroup prologue: LDS = [traversal stack: max_stack x kBlock ints][nodes][tris][qnodes].
 // With kLds the scene's node and triangle arrays are copied into LDS (16 B per lane
 // per step) and the kernel's DScene is pointed at them, so every traversal fetch is
 // a ds_read instead of a dependent L1/L2 load.
@@ -44,16 +44,21 @@ TPT_D int* stage_scene(DScene& s) {
     int* stk = reinterpret_cast<int*>(tpt_smem) + threadIdx.x;
     if (kLds) {
         unsigned char* base = tpt_smem + (size_t)s.max_stack * kBlock * sizeof(int);
-        const int nb = s.nnodes * (int)sizeof(DNode), tb = s.ntri * (int)sizeof(DTri);
+        const int nb = s.nnodes * (int)sizeof(DNode), tb = s.ntri * (int)sizeof(DTri),
+                  qb = s.nqnodes * (int)sizeof(DQNode);
         const uint4* gn = reinterpret_cast<const uint4*>(s.nodes);
         const uint4* gt = reinterpret_cast<const uint4*>(s.tris);
+        const uint4* gq = reinterpret_cast<const uint4*>(s.qnodes);
         uint4* ln = reinterpret_cast<uint4*>(base);
         uint4* lt = reinterpret_cast<uint4*>(base + nb);
+        uint4* lq = reinterpret_cast<uint4*>(base + nb + tb);
         for (int i = threadIdx.x; i < nb / 16; i += kBlock) ln[i] = gn[i];
         for (int i = threadIdx.x; i < tb / 16; i += kBlock) lt[i] = gt[i];
+        for (int i = threadIdx.x; i < qb / 16; i += kBlock) lq[i] = gq[i];
         __syncthreads();
         s.nodes = reinterpret_cast<const DNode*>(base);
         s.tris = reinterpret_cast<const DTri*>(base + nb);
+        s.qnodes = reinterpret_cast<const DQNode*>(base + nb + tb);
     }
     return stk;
 }
@@ -120,10 +125,16 @@ __global__ __launch_bounds__(kBlock, TPT_PT_MINWAVES) void tpt_pt_kernel(DScene 
         uint32_t rs = (uint32_t)((int)i + 1);  // ResetRandom(i + 1), Renderer.cpp:42
         rs = skip_samples(rs, m.type, s.light_draws, q);
         const int base = lane_id() - q;       // first lane of this pixel (Q divides 64)
+#ifdef TPT_STAMPS
+        Stamps st{};
+        st.last = stamp_now();
+#endif
         for (int j0 = 0; j0 < spp; j0 += Q) {
             V3 L = v3s(0.0f);
+            TPT_STAMP(st, 0);
             if (j0 + q < spp) {
-                L = mul(pt_sample(s, px, rs, stk, pk), inv);
+                L = mul(pt_sample(s, px, rs, stk, pk TPT_STAMPS_PASS), inv);
+                TPT_STAMP(st, 11);
                 if (Q > 1) rs = skip_samples(rs, m.type, s.light_draws, Q - 1);
             }
             if (Q == 1) {
@@ -137,6 +148,11 @@ __global__ __launch_bounds__(kBlock, TPT_PT_MINWAVES) void tpt_pt_kernel(DScene 
                 }
             }
         }
+#ifdef TPT_STAMPS
+        TPT_STAMP(st, 0);
+        if (lane_id() == 0)
+            for (int x = 0; x < 12; ++x) atomicAdd(s.dbgc + 8 + x, st.acc[x]);
+#endif
     }
     if (on && q == 0) {
         out[3 * row + 0] = acc.x;
@@ -419,7 +435,7 @@ int launch(tpt_ctx* c, int mode, int spp, int64_t begin, int64_t stride, int64_t
            float* drows, float* dsplat, tpt_stats* st) {
     if (count <= 0) return TPT_OK;
     const int64_t blocks = (count + kBlock - 1) / kBlock;
-    HIP_TRY(c, hipMemsetAsync(c->counters, 0, sizeof(unsigned long long) * 16, c->stream));
+    HIP_TRY(c, hipMemsetAsync(c->counters, 0, sizeof(unsigned long long) * 32, c->stream));
     HIP_TRY(c, hipEventRecord(c->ev0, c->stream));
     const bool lds = c->ds.lds_bytes > 0;
     const size_t shmem = (size_t)c->ds.max_stack * kBlock * sizeof(int) + (size_t)c->ds.lds_bytes;
@@ -445,6 +461,10 @@ int launch(tpt_ctx* c, int mode, int spp, int64_t begin, int64_t stride, int64_t
         HIP_TRY(c, hipStreamWaitEvent(c->stream2, c->ev_fold[0], 0));  // stream2 starts after ev0
         const unsigned pblocks = (unsigned)((count + kBlock - 1) / kBlock);
         const unsigned cblocks = (unsigned)std::min<int64_t>(8192, (count * 24 + kBlock - 1) / kBlock + 1);
+        // connect walks the 4-wide shadow tree with a per-lane stack (shadow_q)
+        DScene dsc = c->ds;
+        dsc.max_stack = std::max(dsc.max_stack, dsc.q_stack);
+        const size_t cshmem = (size_t)dsc.max_stack * kBlock * sizeof(int) + (size_t)dsc.lds_bytes;
         const float inv = 1.0f / spp;
         for (int it = 0; it < spp; ++it) {
             const int b = it & 1;
@@ -468,10 +488,10 @@ int launch(tpt_ctx* c, int mode, int spp, int64_t begin, int64_t stride, int64_t
             HIP_TRY(c, hipEventRecord(c->ev_gen[b], c->stream));
             HIP_TRY(c, hipStreamWaitEvent(c->stream2, c->ev_gen[b], 0));
             if (lds)
-                hipLaunchKernelGGL(tpt_bdpt_conn_kernel<true>, dim3(cblocks), dim3(kBlock), shmem, c->stream2, c->ds, w,
+                hipLaunchKernelGGL(tpt_bdpt_conn_kernel<true>, dim3(cblocks), dim3(kBlock), cshmem, c->stream2, dsc, w,
                                    dsplat);
             else
-                hipLaunchKernelGGL(tpt_bdpt_conn_kernel<false>, dim3(cblocks), dim3(kBlock), shmem, c->stream2, c->ds,
+                hipLaunchKernelGGL(tpt_bdpt_conn_kernel<false>, dim3(cblocks), dim3(kBlock), cshmem, c->stream2, dsc,
                                    w, dsplat);
             hipLaunchKernelGGL(tpt_bdpt_fold_kernel, dim3(pblocks), dim3(kBlock), 0, c->stream2, w, inv);
             HIP_TRY(c, hipEventRecord(c->ev_fold[b], c->stream2));
@@ -484,11 +504,14 @@ int launch(tpt_ctx* c, int mode, int spp, int64_t begin, int64_t stride, int64_t
         w.n = count;
         hipLaunchKernelGGL(tpt_bdpt_out_kernel, dim3(pblocks), dim3(kBlock), 0, c->stream, w, drows, dlist ? 1 : 0);
     } else {
+        DScene dsc = c->ds;  // per-lane shadow_q needs the 4-wide tree's stack depth
+        dsc.max_stack = std::max(dsc.max_stack, dsc.q_stack);
+        const size_t cshmem = (size_t)dsc.max_stack * kBlock * sizeof(int) + (size_t)dsc.lds_bytes;
         if (lds)
-            hipLaunchKernelGGL(tpt_bdpt_kernel<true>, dim3((unsigned)blocks), dim3(kBlock), shmem, c->stream, c->ds,
+            hipLaunchKernelGGL(tpt_bdpt_kernel<true>, dim3((unsigned)blocks), dim3(kBlock), cshmem, c->stream, dsc,
                                spp, begin, stride, count, dlist, drows, dsplat, c->counters);
         else
-            hipLaunchKernelGGL(tpt_bdpt_kernel<false>, dim3((unsigned)blocks), dim3(kBlock), shmem, c->stream, c->ds,
+            hipLaunchKernelGGL(tpt_bdpt_kernel<false>, dim3((unsigned)blocks), dim3(kBlock), cshmem, c->stream, dsc,
                                spp, begin, stride, count, dlist, drows, dsplat, c->counters);
     }
     HIP_TRY(c, hipGetLastError());
@@ -523,6 +546,18 @@ int launch(tpt_ctx* c, int mode, int spp, int64_t begin, int64_t stride, int64_t
         std::fprintf(stderr, "[tpt dbg] bdpt strategies per lane-sample: mean %.2f, wave-max %.2f\n",
                      (double)d[5] / d[7], (double)d[6] / d[7]);
     }
+#ifdef TPT_STAMPS
+    if (mode == TPT_MODE_PT) {
+        unsigned long long d[12];
+        HIP_TRY(c, hipMemcpy(d, c->counters + 16, sizeof(d), hipMemcpyDeviceToHost));
+        static const char* nm[12] = {"loop/fold", "mat_sample", "light sample", "bsdf light-hit", "bsdf geom",
+                                     "bsdf shadow", "bsdf eval", "mat_pdf", "light light-hit", "light shadow",
+                                     "light eval", "skip+tail"};
+        double tot = 0;
+        for (int x = 0; x < 12; ++x) tot += (double)d[x];
+        for (int x = 0; x < 12; ++x) std::fprintf(stderr, "[tpt stamps] %-16s %5.1f%%\n", nm[x], 100.0 * d[x] / tot);
+    }
+#endif
     if (c->ds.dbg & 2) {  // profiling counters (TPT_DEBUG_FLAGS & 2)
         unsigned long long d[8];
         HIP_TRY(c, hipMemcpy(d, c->counters + 8, sizeof(d), hipMemcpyDeviceToHost));
@@ -566,7 +601,7 @@ int tpt_create(int device, tpt_ctx** out) {
         hipEventCreateWithFlags(&c->ev_gen[1], hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_fold[0], hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_fold[1], hipEventDisableTiming) != hipSuccess ||
-        hipMalloc(&c->counters, sizeof(unsigned long long) * 16) != hipSuccess) {
+        hipMalloc(&c->counters, sizeof(unsigned long long) * 32) != hipSuccess) {
         delete c;
         return TPT_E_DEVICE;
     }
@@ -607,14 +642,15 @@ int tpt_upload_scene(tpt_ctx* c, const tpt_scene_desc* d) {
     HostScene hs;
     int rc = build_host_scene(d, hs, c->err);
     if (rc != TPT_OK) return rc;
-    if (hs.max_stack > kStackCap)
-        return fail(c, TPT_E_UNSUPPORTED, "BVH deeper than the LDS traversal stack (" + std::to_string(hs.max_stack) + ")");
+    if (hs.max_stack > kStackCap || hs.q_stack > kStackCap)
+        return fail(c, TPT_E_UNSUPPORTED, "BVH deeper than the LDS traversal stack (" + std::to_string(hs.max_stack) +
+                                              ", " + std::to_string(hs.q_stack) + ")");
     if (hs.nodes.size() > (size_t)0x7fffffff) return fail(c, TPT_E_UNSUPPORTED, "too many BVH nodes");
     std::vector<char> blob;
     size_t o_nodes = push_array(blob, hs.nodes), o_area = push_array(blob, hs.node_area),
            o_tris = push_array(blob, hs.tris), o_trix = push_array(blob, hs.trix), o_sph = push_array(blob, hs.sph),
            o_mats = push_array(blob, hs.mats), o_objs = push_array(blob, hs.objs),
-           o_em = push_array(blob, hs.emitters);
+           o_em = push_array(blob, hs.emitters), o_q = push_array(blob, hs.qnodes);
     if (c->blob) { (void)hipFree(c->blob); c->blob = nullptr; }
     HIP_TRY(c, hipMalloc(&c->blob, blob.size()));
     HIP_TRY(c, hipMemcpy(c->blob, blob.data(), blob.size(), hipMemcpyHostToDevice));
@@ -629,6 +665,8 @@ int tpt_upload_scene(tpt_ctx* c, const tpt_scene_desc* d) {
     ds.mats = (const DMat*)(b + o_mats);
     ds.objs = (const DObj*)(b + o_objs);
     ds.emitters = (const int32_t*)(b + o_em);
+    ds.qnodes = (const DQNode*)(b + o_q);
+    ds.nqnodes = (int)hs.qnodes.size();
     ds.n_emitters = (int)hs.emitters.size();
     // BVHAccel::Sample (1 draw) + Triangle::Sample (2) per mesh emitter, Sphere::Sample (2)
     ds.light_draws = 0;
@@ -642,10 +680,12 @@ int tpt_upload_scene(tpt_ctx* c, const tpt_scene_desc* d) {
     ds.scale = camera_scale(hs.fov);
     for (int k = 0; k < 3; ++k) { ds.eye[k] = hs.eye[k]; ds.bg[k] = hs.bg[k]; }
     ds.max_stack = hs.max_stack;
-    // Stage nodes + triangles in LDS when they fit next to the stack (<= 96 KB per
-    // workgroup keeps >= 1 workgroup per CU; the Cornell presets need ~4 KB).
+    ds.q_stack = hs.q_stack;
+    // Stage nodes + triangles + 4-wide nodes in LDS when they fit in 64 KB (the
+    // Cornell presets need ~6 KB).
     {
-        const size_t sb = hs.nodes.size() * sizeof(DNode) + hs.tris.size() * sizeof(DTri);
+        const size_t sb = hs.nodes.size() * sizeof(DNode) + hs.tris.size() * sizeof(DTri) +
+                          hs.qnodes.size() * sizeof(DQNode);
         const char* no = std::getenv("TPT_NO_LDS");
         ds.lds_bytes = (sb <= 64 * 1024 && !(no && no[0] == '1')) ? (int)sb : 0;
         const char* dbg = std::getenv("TPT_DEBUG_FLAGS");

@@ -21,7 +21,7 @@ namespace tpt {
 #define TPT_D __device__ __forceinline__
 
 constexpr int kBlock = 256;     // threads per workgroup (4 waves)
-constexpr int kStackCap = 40;   // max LDS stack entries per lane (upload rejects deeper trees)
+constexpr int kStackCap = 64;   // max LDS stack entries per lane / per wave packet (upload rejects deeper trees)
 
 // ------------------------------------------------------------------ rays --
 struct Ray {
@@ -46,24 +46,38 @@ struct Hit {
 
 // Bounds3::IntersectP (Bounds3.hpp:92-115): nmin starts at FLT_MIN, std::max /
 // std::min ignore a NaN second argument, hit iff nmax > 0 && nmin <= nmax.
-TPT_D bool box_hit(const DNode& n, const Ray& r) {
+TPT_D bool slab_hit(float x0, float y0, float z0, float x1, float y1, float z1, const Ray& r) {
     float nmin = 1.17549435e-38f, nmax = 3.40282347e+38f;
     {
-        float t1 = (n.bmin[0] - r.o.x) * r.inv.x, t2 = (n.bmax[0] - r.o.x) * r.inv.x;
+        float t1 = (x0 - r.o.x) * r.inv.x, t2 = (x1 - r.o.x) * r.inv.x;
         if (t1 > t2) { float t = t1; t1 = t2; t2 = t; }
         nmin = smax(nmin, t1); nmax = smin(nmax, t2);
     }
     {
-        float t1 = (n.bmin[1] - r.o.y) * r.inv.y, t2 = (n.bmax[1] - r.o.y) * r.inv.y;
+        float t1 = (y0 - r.o.y) * r.inv.y, t2 = (y1 - r.o.y) * r.inv.y;
         if (t1 > t2) { float t = t1; t1 = t2; t2 = t; }
         nmin = smax(nmin, t1); nmax = smin(nmax, t2);
     }
     {
-        float t1 = (n.bmin[2] - r.o.z) * r.inv.z, t2 = (n.bmax[2] - r.o.z) * r.inv.z;
+        float t1 = (z0 - r.o.z) * r.inv.z, t2 = (z1 - r.o.z) * r.inv.z;
         if (t1 > t2) { float t = t1; t1 = t2; t2 = t; }
         nmin = smax(nmin, t1); nmax = smin(nmax, t2);
     }
     return nmax > 0.0f && nmin <= nmax;
+}
+TPT_D bool box_hit(const DNode& n, const Ray& r) {
+    return slab_hit(n.bmin[0], n.bmin[1], n.bmin[2], n.bmax[0], n.bmax[1], n.bmax[2], r);
+}
+TPT_D bool box_hit_q(const DQNode& q, int j, const Ray& r) {
+    return slab_hit(q.bmin[0][j], q.bmin[1][j], q.bmin[2][j], q.bmax[0][j], q.bmax[1][j], q.bmax[2][j], r);
+}
+// The slab test is monotone in the box bounds (tpt_scene_build.cpp: build_q) unless
+// a direction component is +-0 or tiny enough that 1/d overflows: with inv = -inf
+// a box flat at o.x passes while a box [o.x, o.x + w] does not.  Rays with an
+// infinite inv component are walked on the binary tree instead.
+TPT_D bool ray_monotone(const Ray& r) {
+    const float inf = 3.40282347e+38f;
+    return fabs_(r.inv.x) <= inf && fabs_(r.inv.y) <= inf && fabs_(r.inv.z) <= inf;
 }
 
 TPT_D V3 tri_normal(const DTri& t) { return v3(t.nx, t.ny, t.nz); }
@@ -214,6 +228,10 @@ TPT_D bool box_overlap(const DNode& n, V3 lo, V3 hi) {
     return !(n.bmin[0] > hi.x || n.bmax[0] < lo.x || n.bmin[1] > hi.y || n.bmax[1] < lo.y || n.bmin[2] > hi.z ||
              n.bmax[2] < lo.z);
 }
+TPT_D bool box_overlap_q(const DQNode& q, int j, V3 lo, V3 hi) {
+    return !(q.bmin[0][j] > hi.x || q.bmax[0][j] < lo.x || q.bmin[1][j] > hi.y || q.bmax[1][j] < lo.y ||
+             q.bmin[2][j] > hi.z || q.bmax[2][j] < lo.z);
+}
 TPT_D bool shadow_pts(const DScene& s, V3 lc, V3 x, int cull, int* stk) {
     if (s.dbg & 1) return false;  // profiling ablation only
     const double ld2 = dot3(lc - x, lc - x);
@@ -251,6 +269,48 @@ TPT_D bool shadow_pts(const DScene& s, V3 lc, V3 x, int cull, int* stk) {
     return false;
 }
 
+// shadow_pts on the 4-wide tree (same answer, see build_q): one node fetch and four
+// box tests per step instead of one fetch per box.
+TPT_D bool shadow_q(const DScene& s, V3 lc, V3 x, int cull, int* stk) {
+    if (s.dbg & 1) return false;  // profiling ablation only
+    const double ld2 = dot3(lc - x, lc - x);
+    const double thr = ld2 - 1.0f;
+    if (!(thr > 0.0)) return false;  // d2 >= 0 can never be < thr
+    const Ray r = make_ray(lc, normalized(x - lc));
+    if (!ray_monotone(r)) return shadow_pts(s, lc, x, cull, stk);
+    const float T = (float)(sqrt_d(thr) * 1.0001 + 0.01);
+    const V3 e = v3(r.o.x + T * r.d.x, r.o.y + T * r.d.y, r.o.z + T * r.d.z);
+    const float pad = 0.01f + 1e-4f * T;
+    const V3 lo = v3(fminf(r.o.x, e.x) - pad, fminf(r.o.y, e.y) - pad, fminf(r.o.z, e.z) - pad);
+    const V3 hi = v3(fmaxf(r.o.x, e.x) + pad, fmaxf(r.o.y, e.y) + pad, fmaxf(r.o.z, e.z) + pad);
+    int sp = 1;
+    stk[0] = 0;
+    while (sp > 0) {
+        --sp;
+        const DQNode& q = s.qnodes[stk[sp * kBlock]];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int c = q.child[j];
+            if (!box_overlap_q(q, j, lo, hi) || !box_hit_q(q, j, r)) continue;  // empty slots never overlap
+            if (c >= 0) {
+                stk[sp * kBlock] = c;
+                ++sp;
+                continue;
+            }
+            const int prim = -1 - c;
+            double dist;
+            bool h;
+            if (prim < s.ntri) h = tri_test(s.tris[prim], r, cull, dist);
+            else h = sphere_test(s.sph[prim - s.ntri], r, cull, dist);
+            if (h) {
+                const V3 hx = r.o + mul(r.d, (float)dist);
+                if (dot3(hx - lc, hx - lc) < thr) return true;
+            }
+        }
+    }
+    return false;
+}
+
 // ------------------------------------------------------- wave packets --
 // Wave-packet traversal: the 64 lanes of a wave walk ONE depth-first node sequence
 // (reference order: right child popped first) held in a wave-uniform LDS stack of
@@ -278,10 +338,10 @@ TPT_D unsigned long long uni64(unsigned long long v) {
 // Children are box-tested together at their parent (both tests are independent,
 // so they overlap in the pipeline) and the walk descends without a stack round
 // trip; a node's mask holds the lanes whose ray passed that node's own box.
-TPT_D bool shadow_pts_packet(const DScene& s, V3 lc, V3 x, int cull, Packet pk) {
+TPT_D bool shadow_pts_packet(const DScene& s, V3 lc, V3 x, int cull, Packet pk, bool active = true) {
     const double ld2 = dot3(lc - x, lc - x);
     const double thr = ld2 - 1.0f;
-    bool done = !(thr > 0.0);  // done lanes have their answer in `shadowed`
+    bool done = !active || !(thr > 0.0);  // done lanes have their answer in `shadowed`
     bool shadowed = false;
     if (s.dbg & 1) done = true;  // profiling ablation only
     const Ray r = make_ray(lc, normalized(x - lc));
@@ -352,6 +412,82 @@ TPT_D bool shadow_pts_packet(const DScene& s, V3 lc, V3 x, int cull, Packet pk) 
             atomicAdd(s.dbgc + 3, it_leaf);
             atomicAdd(s.dbgc + 5, (unsigned long long)__popcll(act));
         }
+    }
+    return shadowed;
+}
+
+// shadow_pts_packet on the 4-wide tree (same answer per lane, see build_q): per step
+// one wave-uniform node fetch, four box tests per lane, leaf children tested by the
+// lanes whose box passed, interior children pushed with their lane masks.  Lanes
+// whose ray is not monotone (ray_monotone) take the binary walk afterwards.
+TPT_D bool shadow_q_packet(const DScene& s, V3 lc, V3 x, int cull, Packet pk) {
+    const double ld2 = dot3(lc - x, lc - x);
+    const double thr = ld2 - 1.0f;
+    bool done = !(thr > 0.0);  // done lanes have their answer in `shadowed`
+    bool shadowed = false;
+    if (s.dbg & 1) done = true;  // profiling ablation only
+    const Ray r = make_ray(lc, normalized(x - lc));
+    const bool slow = !done && !ray_monotone(r);
+    if (slow) done = true;
+    const float T = (float)(sqrt_d(thr > 0.0 ? thr : 0.0) * 1.0001 + 0.01);
+    const V3 e = v3(r.o.x + T * r.d.x, r.o.y + T * r.d.y, r.o.z + T * r.d.z);
+    const float pad = 0.01f + 1e-4f * T;
+    const V3 lo = v3(fminf(r.o.x, e.x) - pad, fminf(r.o.y, e.y) - pad, fminf(r.o.z, e.z) - pad);
+    const V3 hi = v3(fmaxf(r.o.x, e.x) + pad, fmaxf(r.o.y, e.y) + pad, fmaxf(r.o.z, e.z) + pad);
+    unsigned long long live = uni64(__ballot(!done));
+    if (live != 0) {
+        int sp = 0;
+        int cur = 0;
+        unsigned long long m = live;
+        for (;;) {
+            if (m != 0) {
+                const DQNode& q = s.qnodes[cur];
+                const bool mine = (m >> lane_id()) & 1ull;
+                unsigned long long mk[4];
+                int ch[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    ch[j] = uni(q.child[j]);
+                    mk[j] = uni64(__ballot(mine && box_overlap_q(q, j, lo, hi) && box_hit_q(q, j, r)));
+                }
+                int next = 0;
+                unsigned long long nm = 0;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    if (mk[j] == 0) continue;
+                    if (ch[j] < 0) {
+                        if (((mk[j] >> lane_id()) & 1ull) && !done) {
+                            const int prim = -1 - ch[j];
+                            double dist;
+                            bool h;
+                            if (prim < s.ntri) h = tri_test(s.tris[prim], r, cull, dist);
+                            else h = sphere_test(s.sph[prim - s.ntri], r, cull, dist);
+                            if (h) {
+                                const V3 hx = r.o + mul(r.d, (float)dist);
+                                if (dot3(hx - lc, hx - lc) < thr) { shadowed = true; done = true; }
+                            }
+                        }
+                        live = uni64(__ballot(!done)) & live;
+                    } else if (nm == 0) {
+                        next = ch[j];
+                        nm = mk[j];
+                    } else {
+                        if (lane_id() == __builtin_ctzll(mk[j])) { pk.node[sp] = ch[j]; pk.mask[sp] = mk[j]; }
+                        ++sp;
+                    }
+                }
+                if (live == 0) break;
+                if (nm != 0) { cur = next; m = nm & live; continue; }
+            }
+            if (sp == 0) break;
+            --sp;
+            cur = uni(pk.node[sp]);
+            m = uni64(pk.mask[sp]) & live;
+        }
+    }
+    if (uni64(__ballot(slow)) != 0) {
+        const bool sh = shadow_pts_packet(s, lc, x, cull, pk, slow);
+        if (slow) shadowed = sh;
     }
     return shadowed;
 }
@@ -772,6 +908,35 @@ TPT_D Hit object_hit(const DScene& s, const DObj& o, const Ray& r, int cull, int
 }
 
 // ------------------------------------------------------------------- PT ---
+// Diagnostic build only (-DTPT_STAMPS): wave-level s_memtime stamps that add the
+// cycles of each section of a PT sample into scalar sums, stored once per wave
+// into DScene::dbgc[16..].  Production builds compile these to nothing.
+#ifdef TPT_STAMPS
+struct Stamps {
+    unsigned long long last, acc[12];
+};
+TPT_D unsigned long long stamp_now() {
+    unsigned long long t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
+#define TPT_STAMP(st, i)                          \
+    do {                                          \
+        const unsigned long long t_ = stamp_now(); \
+        (st).acc[i] += t_ - (st).last;            \
+        (st).last = t_;                           \
+    } while (0)
+#define TPT_STAMPS_ARG , Stamps& st
+#define TPT_STAMPS_PASS , st
+#else
+#define TPT_STAMP(st, i) \
+    do {                 \
+    } while (0)
+#define TPT_STAMPS_ARG
+#define TPT_STAMPS_PASS
+#endif
 // The camera hit and its material are invariant over a pixel's spp loop.  Held in
 // registers across the loop they cost ~25 VGPRs at every point of the sample body
 // and push the kernel into scratch spills; instead each lane parks them in LDS
@@ -786,9 +951,8 @@ enum PixSlot {
     kPxX,
     kPxN = kPxX + 3,
     kPxWo = kPxN + 3,
-    kPxKd = kPxWo + 3,
-    kPxIorM = kPxKd + 3,
-    kPxIorMK = kPxIorM + 3,
+    kPxKdM = kPxWo + 3,   // Dieletric: Kd; Metal: ior_m (each type reads only its own)
+    kPxIorMK = kPxKdM + 3,
     kPixSlots = kPxIorMK + 3
 };
 struct PixPark {
@@ -809,8 +973,8 @@ struct PixPark {
         m.type = __float_as_int(p[kPxType * kBlock]);
         m.ior_d = p[kPxIorD * kBlock];
         m.rough = p[kPxRough * kBlock];
-        m.kd = v3(p[kPxKd * kBlock], p[(kPxKd + 1) * kBlock], p[(kPxKd + 2) * kBlock]);
-        m.ior_m = v3(p[kPxIorM * kBlock], p[(kPxIorM + 1) * kBlock], p[(kPxIorM + 2) * kBlock]);
+        m.kd = v3(p[kPxKdM * kBlock], p[(kPxKdM + 1) * kBlock], p[(kPxKdM + 2) * kBlock]);
+        m.ior_m = m.kd;
         m.ior_m_k = v3(p[kPxIorMK * kBlock], p[(kPxIorMK + 1) * kBlock], p[(kPxIorMK + 2) * kBlock]);
         m.em = v3s(0.0f);  // emission is read from the scene where it is used
         return m;
@@ -829,8 +993,7 @@ struct PixPark {
         put3(kPxX, x);
         put3(kPxN, n);
         put3(kPxWo, wo);
-        put3(kPxKd, m.kd);
-        put3(kPxIorM, m.ior_m);
+        put3(kPxKdM, m.type == TPT_METAL ? m.ior_m : m.kd);
         put3(kPxIorMK, m.ior_m_k);
     }
 };
@@ -839,7 +1002,7 @@ struct PixPark {
 // direct lighting from every emitter, then the unconditional `break` (:109).
 // The camera hit is the same for every sample of a pixel (no jitter,
 // SceneRenderingHelper.cpp:16-22): the caller computes it once and parks it in `px`.
-TPT_D V3 pt_sample(const DScene& s, PixPark px, uint32_t& rs, int* stk, Packet pk) {
+TPT_D V3 pt_sample(const DScene& s, PixPark px, uint32_t& rs, int* stk, Packet pk TPT_STAMPS_ARG) {
     V3 result = v3s(0.0f);
     {
         const DMat& dm = s.mats[px.mat_index()];
@@ -847,6 +1010,7 @@ TPT_D V3 pt_sample(const DScene& s, PixPark px, uint32_t& rs, int* stk, Packet p
     }
     float pdf_b;
     V3 wib = mat_sample(px.mat(), px.v(kPxWo), px.v(kPxN), &pdf_b, rs);
+    TPT_STAMP(st, 1);
     for (int li = 0; li < s.n_emitters; ++li) {
         const DObj o = s.objs[s.emitters[li]];
         // DirectLightSampler::sample (PathTracer.cpp:26-40)
@@ -859,12 +1023,14 @@ TPT_D V3 pt_sample(const DScene& s, PixPark px, uint32_t& rs, int* stk, Packet p
         float ct = (float)dot3(pn, -wil);
         float pll = (float)((double)o.pdf * d2 / (double)fabs_(ct));
         V3 ev = v3s(0.0f);
+        TPT_STAMP(st, 2);
         {
             // DirectLightSampler::pdf (PathTracer.cpp:14-24) on the BSDF direction
             const V3 hx0 = px.v(kPxX);
             Ray rb = make_ray(hx0, wib);
             Hit hnc, hb;
             object_hit_nocull_back(s, o, rb, hnc, hb, stk);
+            TPT_STAMP(st, 3);
             float pbl = 0.0f;
             if (hnc.prim >= 0) {
                 V3 hx, hn;
@@ -877,20 +1043,29 @@ TPT_D V3 pt_sample(const DScene& s, PixPark px, uint32_t& rs, int* stk, Packet p
                 if (hb.prim >= 0) {
                     V3 hx, hn;
                     hit_geometry(s, rb, hb, hx, hn);
-                    if (!shadow_pts_packet(s, hx, px.v(kPxX), TPT_CULL_BACK, pk))
+                    TPT_STAMP(st, 4);
+                    const bool sh = shadow_q_packet(s, hx, px.v(kPxX), TPT_CULL_BACK, pk);
+                    TPT_STAMP(st, 5);
+                    if (!sh)
                         ev = ev + divs(eval_bsdf(px.mat(), px.v(kPxWo), wib, px.v(kPxN), true), 1e-4f + pdf_b + pbl);
+                    TPT_STAMP(st, 6);
                 }
             }
         }
         // the light branch (PathTracer.cpp:95-106); plb is pure, so it is computed here
         float plb = mat_pdf(px.mat(), px.v(kPxWo), px.v(kPxN), wil);
+        TPT_STAMP(st, 7);
         if (pll + plb > 0.0f) {
             Ray rl = make_ray(px.v(kPxX), wil);
             Hit hl = object_hit(s, o, rl, TPT_CULL_BACK, stk);
             V3 hx = v3s(0.0f), hn;  // default Intersection::coords when missed (Intersection.hpp:14-21)
             if (hl.prim >= 0) hit_geometry(s, rl, hl, hx, hn);
-            if (!shadow_pts_packet(s, hx, px.v(kPxX), TPT_CULL_BACK, pk))
+            TPT_STAMP(st, 8);
+            const bool sh = shadow_q_packet(s, hx, px.v(kPxX), TPT_CULL_BACK, pk);
+            TPT_STAMP(st, 9);
+            if (!sh)
                 ev = ev + divs(eval_bsdf(px.mat(), px.v(kPxWo), wil, px.v(kPxN), true), 1e-4f + pll + plb);
+            TPT_STAMP(st, 10);
         }
         result = result + ev * load_mat(s, o.mat).em;
     }

@@ -27,6 +27,17 @@ struct DNode {
 };
 static const int32_t kEmptyLeaf = (int32_t)0x80000000;
 
+// 128 B: a 4-wide node for shadow (any-hit) queries, made by collapsing two levels
+// of the binary tree (tpt_scene_build.cpp: build_qnodes).  Child j's box is the
+// binary node's own box; child >= 0 is another DQNode, child < 0 a leaf as in
+// DNode::a, kEmptyLeaf an unused slot (its box is inverted and never overlaps).
+struct DQNode {
+    float bmin[3][4];  // [axis][child]
+    float bmax[3][4];
+    int32_t child[4];
+    int32_t pad[4];
+};
+
 // 48 B, read as three float4: (v0, n.x) (e1, n.y) (e2, n.z) -- Triangle.hpp:46-50
 struct DTri {
     float v0[3];
@@ -83,6 +94,7 @@ struct DScene {
     const DMat* mats;
     const DObj* objs;
     const int32_t* emitters;  // Scene::m_emissionObjects (object ids)
+    const DQNode* qnodes;     // 4-wide shadow tree, root at 0
     int32_t n_emitters;
     int32_t light_draws;  // XorShift draws of one DirectLightSampler::sample pass over all emitters
     int32_t ntri;
@@ -94,8 +106,10 @@ struct DScene {
     float scale;  // CalculateScale(fov) (SceneRenderingHelper.cpp:12-14), host-computed
     float eye[3];
     float bg[3];
-    int32_t max_stack;  // deepest traversal stack any ray can need (LDS stack entries per lane)
-    int32_t lds_bytes;  // bytes of nodes + triangles staged in LDS per workgroup (0 = read from HBM/L2)
+    int32_t nqnodes;
+    int32_t max_stack;  // LDS stack entries per lane a binary-tree walk can need (depth + 1)
+    int32_t q_stack;    // ... and a per-lane walk of the 4-wide shadow tree (3 per level + 1)
+    int32_t lds_bytes;  // bytes of nodes + triangles + qnodes staged in LDS per workgroup (0 = read from HBM/L2)
     int32_t dbg;        // ablation switches for profiling only (TPT_DEBUG_FLAGS); 0 in production
     unsigned long long* dbgc;  // profiling counters (TPT_DEBUG_FLAGS & 2)
 };

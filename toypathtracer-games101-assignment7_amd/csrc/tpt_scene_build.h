@@ -10,6 +10,7 @@ namespace tpt {
 
 struct HostScene {
     std::vector<DNode> nodes;
+    std::vector<DQNode> qnodes;
     std::vector<float> node_area;
     std::vector<DTri> tris;
     std::vector<DTriX> trix;
@@ -23,6 +24,7 @@ struct HostScene {
     float bg[3] = {0, 0, 0};
     double fov = 40.0;
     int max_stack = 1;
+    int q_stack = 1;
 };
 
 int build_host_scene(const tpt_scene_desc* d, HostScene& hs, std::string& err);
