@@ -63,7 +63,7 @@ TPT_D bool slab_hit(float x0, float y0, float z0, float x1, float y1, float z1, 
         if (t1 > t2) { float t = t1; t1 = t2; t2 = t; }
         nmin = smax(nmin, t1); nmax = smin(nmax, t2);
     }
-    return nmax > 0.0f && nmin <= nmax;
+    return (nmax > 0.0f) & (nmin <= nmax);
 }
 TPT_D bool box_hit(const DNode& n, const Ray& r) {
     return slab_hit(n.bmin[0], n.bmin[1], n.bmin[2], n.bmax[0], n.bmax[1], n.bmax[2], r);
@@ -84,7 +84,7 @@ TPT_D V3 tri_normal(const DTri& t) { return v3(t.nx, t.ny, t.nz); }
 
 // Triangle::GetIntersection (Triangle.cpp:77-118): culling on the f64 sign of
 // dot(d, n), then f64 Moller-Trumbore with |det| < EPSILON(1e-4f) rejection.
-TPT_D bool tri_test(const DTri& t, const Ray& r, int cull, double& dist) {
+TPT_D bool tri_test(const DTri t, const Ray& r, int cull, double& dist) {  // by value: all 48 B load up front
     V3 n = tri_normal(t);
     if (cull == TPT_CULL_BACK) {
         if (dot3(r.d, n) > 0) return false;
@@ -225,12 +225,13 @@ TPT_D PTV scene_intersect(const DScene& s, const Ray& r, int cull, int* stk) {
 // contain one and are skipped.  Box tests themselves are the reference's, so the
 // set of reachable primitives is unchanged.
 TPT_D bool box_overlap(const DNode& n, V3 lo, V3 hi) {
-    return !(n.bmin[0] > hi.x || n.bmax[0] < lo.x || n.bmin[1] > hi.y || n.bmax[1] < lo.y || n.bmin[2] > hi.z ||
-             n.bmax[2] < lo.z);
+    return !((n.bmin[0] > hi.x) | (n.bmax[0] < lo.x) | (n.bmin[1] > hi.y) | (n.bmax[1] < lo.y) | (n.bmin[2] > hi.z) |
+             (n.bmax[2] < lo.z));
 }
+// Branch-free (bitwise) so the six compares never become a chain of branches.
 TPT_D bool box_overlap_q(const DQNode& q, int j, V3 lo, V3 hi) {
-    return !(q.bmin[0][j] > hi.x || q.bmax[0][j] < lo.x || q.bmin[1][j] > hi.y || q.bmax[1][j] < lo.y ||
-             q.bmin[2][j] > hi.z || q.bmax[2][j] < lo.z);
+    return !((q.bmin[0][j] > hi.x) | (q.bmax[0][j] < lo.x) | (q.bmin[1][j] > hi.y) | (q.bmax[1][j] < lo.y) |
+             (q.bmin[2][j] > hi.z) | (q.bmax[2][j] < lo.z));
 }
 TPT_D bool shadow_pts(const DScene& s, V3 lc, V3 x, int cull, int* stk) {
     if (s.dbg & 1) return false;  // profiling ablation only
@@ -287,11 +288,14 @@ TPT_D bool shadow_q(const DScene& s, V3 lc, V3 x, int cull, int* stk) {
     stk[0] = 0;
     while (sp > 0) {
         --sp;
-        const DQNode& q = s.qnodes[stk[sp * kBlock]];
+        const DQNode q = s.qnodes[stk[sp * kBlock]];
+        bool hit[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) hit[j] = box_overlap_q(q, j, lo, hi) & box_hit_q(q, j, r);  // empty slots never overlap
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const int c = q.child[j];
-            if (!box_overlap_q(q, j, lo, hi) || !box_hit_q(q, j, r)) continue;  // empty slots never overlap
+            if (!hit[j]) continue;
             if (c >= 0) {
                 stk[sp * kBlock] = c;
                 ++sp;
@@ -358,7 +362,7 @@ TPT_D bool shadow_pts_packet(const DScene& s, V3 lc, V3 x, int cull, Packet pk, 
     unsigned long long m;
     {
         const DNode n = s.nodes[0];
-        m = uni64(__ballot(!done && box_overlap(n, lo, hi) && box_hit(n, r)));
+        m = uni64(__ballot(!done & box_overlap(n, lo, hi) & box_hit(n, r)));
     }
     for (;;) {
         ++it_all;
@@ -368,8 +372,8 @@ TPT_D bool shadow_pts_packet(const DScene& s, V3 lc, V3 x, int cull, Packet pk, 
                 const DNode L = s.nodes[n.a];
                 const DNode R = s.nodes[n.b];
                 const bool mine = (m >> lane_id()) & 1ull;
-                const bool hl = mine && box_overlap(L, lo, hi) && box_hit(L, r);
-                const bool hr = mine && box_overlap(R, lo, hi) && box_hit(R, r);
+                const bool hl = mine & box_overlap(L, lo, hi) & box_hit(L, r);
+                const bool hr = mine & box_overlap(R, lo, hi) & box_hit(R, r);
                 const unsigned long long ml = uni64(__ballot(hl)), mr = uni64(__ballot(hr));
                 if (mr != 0) {  // right subtree first (BVH.cpp:129-132), left deferred
                     if (ml != 0) {
@@ -435,20 +439,23 @@ TPT_D bool shadow_q_packet(const DScene& s, V3 lc, V3 x, int cull, Packet pk) {
     const V3 lo = v3(fminf(r.o.x, e.x) - pad, fminf(r.o.y, e.y) - pad, fminf(r.o.z, e.z) - pad);
     const V3 hi = v3(fmaxf(r.o.x, e.x) + pad, fmaxf(r.o.y, e.y) + pad, fmaxf(r.o.z, e.z) + pad);
     unsigned long long live = uni64(__ballot(!done));
+    unsigned long long it_all = 0, it_leaf = 0;
     if (live != 0) {
         int sp = 0;
         int cur = 0;
         unsigned long long m = live;
         for (;;) {
             if (m != 0) {
-                const DQNode& q = s.qnodes[cur];
+                ++it_all;
+                const DQNode q = s.qnodes[cur];  // one 128-B fetch, all loads in flight together
                 const bool mine = (m >> lane_id()) & 1ull;
                 unsigned long long mk[4];
                 int ch[4];
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     ch[j] = uni(q.child[j]);
-                    mk[j] = uni64(__ballot(mine && box_overlap_q(q, j, lo, hi) && box_hit_q(q, j, r)));
+                    const bool h = mine & box_overlap_q(q, j, lo, hi) & box_hit_q(q, j, r);
+                    mk[j] = uni64(__ballot(h));
                 }
                 int next = 0;
                 unsigned long long nm = 0;
@@ -456,7 +463,12 @@ TPT_D bool shadow_q_packet(const DScene& s, V3 lc, V3 x, int cull, Packet pk) {
                 for (int j = 0; j < 4; ++j) {
                     if (mk[j] == 0) continue;
                     if (ch[j] < 0) {
+                        ++it_leaf;
+#ifdef TPT_ABL_NOLEAF
+                        if (false) {
+#else
                         if (((mk[j] >> lane_id()) & 1ull) && !done) {
+#endif
                             const int prim = -1 - ch[j];
                             double dist;
                             bool h;
@@ -483,6 +495,15 @@ TPT_D bool shadow_q_packet(const DScene& s, V3 lc, V3 x, int cull, Packet pk) {
             --sp;
             cur = uni(pk.node[sp]);
             m = uni64(pk.mask[sp]) & live;
+        }
+    }
+    if (s.dbg & 2) {
+        const unsigned long long act = __ballot(1);
+        if (lane_id() == __builtin_ctzll(act)) {
+            atomicAdd(s.dbgc + 0, 1ull);
+            atomicAdd(s.dbgc + 1, it_all);
+            atomicAdd(s.dbgc + 3, it_leaf);
+            atomicAdd(s.dbgc + 5, (unsigned long long)__popcll(act));
         }
     }
     if (uni64(__ballot(slow)) != 0) {
@@ -514,8 +535,8 @@ TPT_D Hit traverse_packet(const DScene& s, int root, const Ray& r, int cull, Pac
                 const DNode L = s.nodes[n.a];
                 const DNode R = s.nodes[n.b];
                 const bool mine = (m >> lane_id()) & 1ull;
-                const bool hl = mine && box_hit(L, r);
-                const bool hr = mine && box_hit(R, r);
+                const bool hl = mine & box_hit(L, r);
+                const bool hr = mine & box_hit(R, r);
                 const unsigned long long ml = uni64(__ballot(hl)), mr = uni64(__ballot(hr));
                 if (mr != 0) {
                     if (ml != 0) {
