@@ -71,6 +71,22 @@ TPT_D bool box_hit(const DNode& n, const Ray& r) {
 TPT_D bool box_hit_q(const DQNode& q, int j, const Ray& r) {
     return slab_hit(q.bmin[0][j], q.bmin[1][j], q.bmin[2][j], q.bmax[0][j], q.bmax[1][j], q.bmax[2][j], r);
 }
+// slab_hit for a ray with finite inv (ray_monotone): (b - o) * inv is then never
+// NaN, so std::max/std::min equal the hardware max/min and the swap is a min/max
+// pair (a +-0 difference cannot change `nmax > 0` or `nmin <= nmax`).  Same
+// decision as slab_hit, half the instructions.
+TPT_D bool slab_hit_finite(float x0, float y0, float z0, float x1, float y1, float z1, const Ray& r) {
+    const float ax = (x0 - r.o.x) * r.inv.x, bx = (x1 - r.o.x) * r.inv.x;
+    const float ay = (y0 - r.o.y) * r.inv.y, by = (y1 - r.o.y) * r.inv.y;
+    const float az = (z0 - r.o.z) * r.inv.z, bz = (z1 - r.o.z) * r.inv.z;
+    const float nmin = fmaxf(fmaxf(1.17549435e-38f, fminf(ax, bx)), fmaxf(fminf(ay, by), fminf(az, bz)));
+    const float nmax = fminf(fminf(3.40282347e+38f, fmaxf(ax, bx)), fminf(fmaxf(ay, by), fmaxf(az, bz)));
+    return (nmax > 0.0f) & (nmin <= nmax);
+}
+TPT_D bool box_hit_q_finite(const DQNode& q, int j, const Ray& r) {
+    return slab_hit_finite(q.bmin[0][j], q.bmin[1][j], q.bmin[2][j], q.bmax[0][j], q.bmax[1][j], q.bmax[2][j], r);
+}
+
 // The slab test is monotone in the box bounds (tpt_scene_build.cpp: build_q) unless
 // a direction component is +-0 or tiny enough that 1/d overflows: with inv = -inf
 // a box flat at o.x passes while a box [o.x, o.x + w] does not.  Rays with an
@@ -291,7 +307,7 @@ TPT_D bool shadow_q(const DScene& s, V3 lc, V3 x, int cull, int* stk) {
         const DQNode q = s.qnodes[stk[sp * kBlock]];
         bool hit[4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) hit[j] = box_overlap_q(q, j, lo, hi) & box_hit_q(q, j, r);  // empty slots never overlap
+        for (int j = 0; j < 4; ++j) hit[j] = box_overlap_q(q, j, lo, hi) & box_hit_q_finite(q, j, r);  // empty slots never overlap
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const int c = q.child[j];
@@ -433,7 +449,8 @@ TPT_D bool shadow_q_packet(const DScene& s, V3 lc, V3 x, int cull, Packet pk) {
     const Ray r = make_ray(lc, normalized(x - lc));
     const bool slow = !done && !ray_monotone(r);
     if (slow) done = true;
-    const float T = (float)(sqrt_d(thr > 0.0 ? thr : 0.0) * 1.0001 + 0.01);
+    // segment-culling bound only (no exactness role): f32 sqrt with a margin
+    const float T = sqrt_f((float)(thr > 0.0 ? thr : 0.0)) * 1.0002f + 0.02f;
     const V3 e = v3(r.o.x + T * r.d.x, r.o.y + T * r.d.y, r.o.z + T * r.d.z);
     const float pad = 0.01f + 1e-4f * T;
     const V3 lo = v3(fminf(r.o.x, e.x) - pad, fminf(r.o.y, e.y) - pad, fminf(r.o.z, e.z) - pad);
@@ -454,7 +471,7 @@ TPT_D bool shadow_q_packet(const DScene& s, V3 lc, V3 x, int cull, Packet pk) {
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     ch[j] = uni(q.child[j]);
-                    const bool h = mine & box_overlap_q(q, j, lo, hi) & box_hit_q(q, j, r);
+                    const bool h = mine & box_overlap_q(q, j, lo, hi) & box_hit_q_finite(q, j, r);
                     mk[j] = uni64(__ballot(h));
                 }
                 int next = 0;
