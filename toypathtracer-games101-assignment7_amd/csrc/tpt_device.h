@@ -86,6 +86,13 @@ TPT_D bool slab_hit_finite(float x0, float y0, float z0, float x1, float y1, flo
 TPT_D bool box_hit_q_finite(const DQNode& q, int j, const Ray& r) {
     return slab_hit_finite(q.bmin[0][j], q.bmin[1][j], q.bmin[2][j], q.bmax[0][j], q.bmax[1][j], q.bmax[2][j], r);
 }
+// kFin: every ray of the (sub)wave has a finite inv (wave_finite), so the NaN-free
+// form gives the same decision.
+template <bool kFin>
+TPT_D bool box_hit_t(const DNode& n, const Ray& r) {
+    return kFin ? slab_hit_finite(n.bmin[0], n.bmin[1], n.bmin[2], n.bmax[0], n.bmax[1], n.bmax[2], r)
+                : slab_hit(n.bmin[0], n.bmin[1], n.bmin[2], n.bmax[0], n.bmax[1], n.bmax[2], r);
+}
 
 // The slab test is monotone in the box bounds (tpt_scene_build.cpp: build_q) unless
 // a direction component is +-0 or tiny enough that 1/d overflows: with inv = -inf
@@ -95,6 +102,9 @@ TPT_D bool ray_monotone(const Ray& r) {
     const float inf = 3.40282347e+38f;
     return fabs_(r.inv.x) <= inf && fabs_(r.inv.y) <= inf && fabs_(r.inv.z) <= inf;
 }
+// True when every active lane's ray has a finite inv: the walk can then use the
+// NaN-free slab test (wave-uniform, so the choice costs no divergence).
+TPT_D bool wave_finite(const Ray& r) { return __ballot(!ray_monotone(r)) == 0; }
 
 TPT_D V3 tri_normal(const DTri& t) { return v3(t.nx, t.ny, t.nz); }
 
@@ -157,7 +167,8 @@ TPT_D bool sphere_test(const DSphere& s, const Ray& r, int cull, double& dist) {
 // BVHAccel::Intersect (BVH.cpp:103-143) from `root`, both levels spliced
 // (tpt_scene.h).  Same pop order (right child first), strict `>` on the f64
 // distance, so ties resolve exactly as in the reference.
-TPT_D Hit traverse(const DScene& s, int root, const Ray& r, int cull, int* stk) {
+template <bool kFin>
+TPT_D Hit traverse_t(const DScene& s, int root, const Ray& r, int cull, int* stk) {
     Hit best;
     best.prim = -1;
     best.dist = 0.0;
@@ -169,7 +180,7 @@ TPT_D Hit traverse(const DScene& s, int root, const Ray& r, int cull, int* stk) 
         --sp;
         const int ni = stk[sp * kBlock];
         const DNode n = s.nodes[ni];
-        if (!box_hit(n, r)) continue;
+        if (!box_hit_t<kFin>(n, r)) continue;
         if (n.a >= 0) {
             stk[sp * kBlock] = n.a;
             stk[(sp + 1) * kBlock] = n.b;
@@ -188,6 +199,9 @@ TPT_D Hit traverse(const DScene& s, int root, const Ray& r, int cull, int* stk) 
         }
     }
     return best;
+}
+TPT_D Hit traverse(const DScene& s, int root, const Ray& r, int cull, int* stk) {
+    return wave_finite(r) ? traverse_t<true>(s, root, r, cull, stk) : traverse_t<false>(s, root, r, cull, stk);
 }
 
 // Intersection fields of a hit (Triangle.cpp:109-114, Sphere.cpp:30-36)
@@ -249,23 +263,14 @@ TPT_D bool box_overlap_q(const DQNode& q, int j, V3 lo, V3 hi) {
     return !((q.bmin[0][j] > hi.x) | (q.bmax[0][j] < lo.x) | (q.bmin[1][j] > hi.y) | (q.bmax[1][j] < lo.y) |
              (q.bmin[2][j] > hi.z) | (q.bmax[2][j] < lo.z));
 }
-TPT_D bool shadow_pts(const DScene& s, V3 lc, V3 x, int cull, int* stk) {
-    if (s.dbg & 1) return false;  // profiling ablation only
-    const double ld2 = dot3(lc - x, lc - x);
-    const double thr = ld2 - 1.0f;
-    if (!(thr > 0.0)) return false;  // d2 >= 0 can never be < thr
-    const Ray r = make_ray(lc, normalized(x - lc));
-    const float T = (float)(sqrt_d(thr) * 1.0001 + 0.01);
-    const V3 e = v3(r.o.x + T * r.d.x, r.o.y + T * r.d.y, r.o.z + T * r.d.z);
-    const float pad = 0.01f + 1e-4f * T;
-    const V3 lo = v3(fminf(r.o.x, e.x) - pad, fminf(r.o.y, e.y) - pad, fminf(r.o.z, e.z) - pad);
-    const V3 hi = v3(fmaxf(r.o.x, e.x) + pad, fmaxf(r.o.y, e.y) + pad, fmaxf(r.o.z, e.z) + pad);
+template <bool kFin>
+TPT_D bool shadow_pts_walk(const DScene& s, const Ray& r, V3 lc, double thr, V3 lo, V3 hi, int cull, int* stk) {
     int sp = 1;
     stk[0] = 0;
     while (sp > 0) {
         --sp;
         const DNode n = s.nodes[stk[sp * kBlock]];
-        if (!box_overlap(n, lo, hi) || !box_hit(n, r)) continue;
+        if (!(box_overlap(n, lo, hi) & box_hit_t<kFin>(n, r))) continue;
         if (n.a >= 0) {
             stk[sp * kBlock] = n.a;
             stk[(sp + 1) * kBlock] = n.b;
@@ -284,6 +289,20 @@ TPT_D bool shadow_pts(const DScene& s, V3 lc, V3 x, int cull, int* stk) {
         }
     }
     return false;
+}
+TPT_D bool shadow_pts(const DScene& s, V3 lc, V3 x, int cull, int* stk) {
+    if (s.dbg & 1) return false;  // profiling ablation only
+    const double ld2 = dot3(lc - x, lc - x);
+    const double thr = ld2 - 1.0f;
+    if (!(thr > 0.0)) return false;  // d2 >= 0 can never be < thr
+    const Ray r = make_ray(lc, normalized(x - lc));
+    const float T = sqrt_f((float)thr) * 1.0002f + 0.02f;  // segment-culling bound only
+    const V3 e = v3(r.o.x + T * r.d.x, r.o.y + T * r.d.y, r.o.z + T * r.d.z);
+    const float pad = 0.01f + 1e-4f * T;
+    const V3 lo = v3(fminf(r.o.x, e.x) - pad, fminf(r.o.y, e.y) - pad, fminf(r.o.z, e.z) - pad);
+    const V3 hi = v3(fmaxf(r.o.x, e.x) + pad, fmaxf(r.o.y, e.y) + pad, fmaxf(r.o.z, e.z) + pad);
+    return wave_finite(r) ? shadow_pts_walk<true>(s, r, lc, thr, lo, hi, cull, stk)
+                          : shadow_pts_walk<false>(s, r, lc, thr, lo, hi, cull, stk);
 }
 
 // shadow_pts on the 4-wide tree (same answer, see build_q): one node fetch and four
@@ -902,23 +921,14 @@ struct Hit2 {
 };
 // NoCull and CullBack closest hits of one ray against one emitter object, one
 // traversal (same node order, same strict `>` tie rule for each result).
-TPT_D void object_hit_nocull_back(const DScene& s, const DObj& o, const Ray& r, Hit& hn, Hit& hb, int* stk) {
-    hn.prim = hb.prim = -1;
-    hn.dist = hb.dist = 0.0;
-    if (o.kind != TPT_OBJ_MESH) {
-        double d;
-        const DSphere sp = s.sph[o.sphere_prim - s.ntri];
-        if (sphere_test(sp, r, TPT_NO_CULL, d)) { hn.prim = o.sphere_prim; hn.dist = d; }
-        if (sphere_test(sp, r, TPT_CULL_BACK, d)) { hb.prim = o.sphere_prim; hb.dist = d; }
-        return;
-    }
-    if (o.root < 0) return;
+template <bool kFin>
+TPT_D void mesh_hit_nocull_back(const DScene& s, int root, const Ray& r, Hit& hn, Hit& hb, int* stk) {
     int sp = 1;
-    stk[0] = o.root;
+    stk[0] = root;
     while (sp > 0) {
         --sp;
         const DNode n = s.nodes[stk[sp * kBlock]];
-        if (!box_hit(n, r)) continue;
+        if (!box_hit_t<kFin>(n, r)) continue;
         if (n.a >= 0) {
             stk[sp * kBlock] = n.a;
             stk[(sp + 1) * kBlock] = n.b;
@@ -933,6 +943,20 @@ TPT_D void object_hit_nocull_back(const DScene& s, const DObj& o, const Ray& r, 
         if (hn.prim < 0 || hn.dist > d) { hn.prim = prim; hn.dist = d; }
         if (!(dot3(r.d, tri_normal(t)) > 0) && (hb.prim < 0 || hb.dist > d)) { hb.prim = prim; hb.dist = d; }
     }
+}
+TPT_D void object_hit_nocull_back(const DScene& s, const DObj& o, const Ray& r, Hit& hn, Hit& hb, int* stk) {
+    hn.prim = hb.prim = -1;
+    hn.dist = hb.dist = 0.0;
+    if (o.kind != TPT_OBJ_MESH) {
+        double d;
+        const DSphere sp = s.sph[o.sphere_prim - s.ntri];
+        if (sphere_test(sp, r, TPT_NO_CULL, d)) { hn.prim = o.sphere_prim; hn.dist = d; }
+        if (sphere_test(sp, r, TPT_CULL_BACK, d)) { hb.prim = o.sphere_prim; hb.dist = d; }
+        return;
+    }
+    if (o.root < 0) return;
+    if (wave_finite(r)) mesh_hit_nocull_back<true>(s, o.root, r, hn, hb, stk);
+    else mesh_hit_nocull_back<false>(s, o.root, r, hn, hb, stk);
 }
 
 TPT_D Hit object_hit(const DScene& s, const DObj& o, const Ray& r, int cull, int* stk) {
