@@ -39,6 +39,7 @@ constexpr float kCamRayPdf = (float)10.0;     // CAMERA_RAY_PDF (BDPT.cpp:8)
 struct BVert {
     V3 x, N;
     int type, prim;
+    int mat;       // material of prim (-1 for the camera / background), resolved once at generation
     float pdf;
     V3 alpha;
     float q1, q8;  // safe_div(rev * rr, pdf) for rr = 1 and rr = .8 (rev: reverse pdf)
@@ -61,26 +62,26 @@ TPT_D float srpdf_to_area(float sr, int t1, V3 x1, V3 n1, int t2, V3 x2, V3 n2) 
 }
 
 // PathVertex::EvalPdfOnSolidAngle (BDPT.cpp:332-351); `pre` = Pre().Position()
-TPT_D float eval_pdf_sa(const DScene& s, int type, int prim, V3 x, V3 N, V3 pre, V3 dir) {
+TPT_D float eval_pdf_sa(const DScene& s, int type, int mat, V3 x, V3 N, V3 pre, V3 dir) {
     const V3 n = normal_of(type, N);
     float c = (float)dabs_(dot3(dir, n));
     if (type == T_LIGHT) return safe_div(cosine_pdf(n, dir), c);
     if (type == T_CAM) return kCamRayPdf;
     if (c == 0.0f) return 0.0f;
     V3 wo = normalized(pre - x);
-    return safe_div(mat_pdf(load_mat(s, prim_mat(s, prim)), wo, n, dir), c);
+    return safe_div(mat_pdf(load_mat(s, mat), wo, n, dir), c);
 }
 // PathVertex::EvalBsdfOnSolidAngle (BDPT.cpp:317-330)
-TPT_D V3 eval_bsdf_sa(const DScene& s, int type, int prim, V3 x, V3 N, V3 pre, V3 dir) {
+TPT_D V3 eval_bsdf_sa(const DScene& s, int type, int mat, V3 x, V3 N, V3 pre, V3 dir) {
     if (type == T_LIGHT || type == T_CAM) return v3s(1.0f);
-    return eval_bsdf(load_mat(s, prim_mat(s, prim)), normalized(pre - x), dir, normal_of(type, N), false);
+    return eval_bsdf(load_mat(s, mat), normalized(pre - x), dir, normal_of(type, N), false);
 }
 // Append's pdf for `v` appended after `last` (whose predecessor is at `pre`), before
 // the RR factor (BDPT.cpp:154-158).
-TPT_D float append_pdf(const DScene& s, int ltype, int lprim, V3 lx, V3 lN, V3 pre, int vtype, V3 vx, V3 vN) {
+TPT_D float append_pdf(const DScene& s, int ltype, int lmat, V3 lx, V3 lN, V3 pre, int vtype, V3 vx, V3 vN) {
     float d2;
     V3 wi = normalize_len2(vx - lx, &d2);
-    float sr = eval_pdf_sa(s, ltype, lprim, lx, lN, pre, wi);
+    float sr = eval_pdf_sa(s, ltype, lmat, lx, lN, pre, wi);
     return srpdf_to_area(sr, ltype, lx, lN, vtype, vx, vN);
 }
 TPT_D float rr_of(int count) { return count > 4 ? .8f : 1.f; }
@@ -96,7 +97,7 @@ TPT_D bool shadow_v(const DScene& s, const BVert& v1, const BVert& v2, Packet pk
     V3 atob = v2.x - v1.x;
     bool test = true;
     int cull = TPT_CULL_BACK;
-    if (v1.prim >= 0 && v2.prim != v1.prim && s.mats[prim_mat(s, v1.prim)].type == TPT_TRANSPARENT) {
+    if (v1.prim >= 0 && v2.prim != v1.prim && s.mats[v1.mat].type == TPT_TRANSPARENT) {
         if (dot3(atob, v1.N) < 0.0f) cull = TPT_CULL_FRONT;
     } else if (v1.prim >= 0 && dot3(atob, v1.N) < 0.0f) {
         test = false;  // fast path "not shadowed" (Scene.cpp:71-74)
@@ -123,7 +124,7 @@ TPT_D int fill_path(const DScene& s, BVert* P, int start, uint32_t& rs, Packet p
         BVert cur = P[i];
         if (cur.type == T_BG) break;
         V3 wo = normalized(P[i - 1].x - cur.x);
-        const Mat m = load_mat(s, prim_mat(s, cur.prim));
+        const Mat m = load_mat(s, cur.mat);
         float raw;
         V3 wi = mat_sample(m, wo, cur.N, &raw, rs);
         const float rr = i > 4 ? .8f : 1.f;
@@ -138,6 +139,7 @@ TPT_D int fill_path(const DScene& s, BVert* P, int start, uint32_t& rs, Packet p
         V3 bsdf = eval_bsdf(m, wo, wi, cur.N, false);
         BVert nx;
         nx.x = it.x; nx.N = it.N; nx.type = it.type; nx.prim = it.prim;
+        nx.mat = it.prim >= 0 ? prim_mat(s, it.prim) : -1;
         nx.pdf = pdf * rr;
         nx.alpha = divs(cur.alpha * safe_div(bsdf, sr), rr);
         nx.q1 = nx.q8 = 0.0f;
@@ -152,7 +154,7 @@ TPT_D int fill_path(const DScene& s, BVert* P, int start, uint32_t& rs, Packet p
 TPT_D void path_rev(const DScene& s, BVert* P, int count) {
     for (int j = 0; j + 2 < count; ++j) {
         const BVert& a = P[j + 1];
-        const float rev = append_pdf(s, a.type, a.prim, a.x, a.N, P[j + 2].x, P[j].type, P[j].x, P[j].N);
+        const float rev = append_pdf(s, a.type, a.mat, a.x, a.N, P[j + 2].x, P[j].type, P[j].x, P[j].N);
         P[j].q1 = safe_div(rev * 1.f, P[j].pdf);
         P[j].q8 = safe_div(rev * .8f, P[j].pdf);
     }
@@ -162,7 +164,7 @@ TPT_D void path_rev(const DScene& s, BVert* P, int count) {
 // Paths are read through an accessor P: P::cam(j), P::lit(j) return vertex records,
 // P::camq / P::litq the cached MIS factors (rr .8 when `r8`).
 template <class P, bool kPacket>
-TPT_D V3 path_weight(const DScene& s, const P& paths, int sl, int tl, Packet pk, int* stk) {
+TPT_D V3 path_weight(const DScene& s, const P& paths, int sl, int tl, Packet pk, int* stk TPT_STAMPS_ARG) {
     const int z = tl - 1;
     const BVert cz = paths.cam(z);
     if (cz.type == T_BG) return sl == 0 ? cz.alpha * v3(s.bg[0], s.bg[1], s.bg[2]) : v3s(0.0f);
@@ -170,21 +172,25 @@ TPT_D V3 path_weight(const DScene& s, const P& paths, int sl, int tl, Packet pk,
     if (sl != 0 && ly.type == T_BG) return v3s(0.0f);
     const V3 cpre = z >= 1 ? paths.cam(z - 1).x : cz.x;
     const V3 lpre = sl >= 2 ? paths.lit(sl - 2).x : ly.x;
+    TPT_STAMP(st, 1);
     V3 cst;
     if (sl == 0) {
         V3 wi = normalized(cpre - cz.x);
         V3 em = v3s(0.0f);  // PathVertex::Emission (BDPT.hpp:119-128)
-        if (cz.prim >= 0) em = load_mat(s, prim_mat(s, cz.prim)).em;
+        if (cz.prim >= 0) em = load_mat(s, cz.mat).em;
         cst = mul(em, (float)dot3(normal_of(cz.type, cz.N), wi));
         if (dot3(em, em) == 0.0f) return v3s(0.0f);
     } else {
         float d2;
         V3 dir = normalize_len2(cz.x - ly.x, &d2);
-        if (shadow_v<kPacket>(s, cz, ly, pk, stk)) return v3s(0.0f);
-        V3 fl = eval_bsdf_sa(s, ly.type, ly.prim, ly.x, ly.N, lpre, dir);
-        V3 fc = eval_bsdf_sa(s, cz.type, cz.prim, cz.x, cz.N, cpre, -dir);
+        const bool shadowed = shadow_v<kPacket>(s, cz, ly, pk, stk);
+        TPT_STAMP(st, 2);
+        if (shadowed) return v3s(0.0f);
+        V3 fl = eval_bsdf_sa(s, ly.type, ly.mat, ly.x, ly.N, lpre, dir);
+        V3 fc = eval_bsdf_sa(s, cz.type, cz.mat, cz.x, cz.N, cpre, -dir);
         cst = mul(fl * fc, (float)dabs_(dot3(normal_of(ly.type, ly.N), dir) * dot3(normal_of(cz.type, cz.N), -dir) / (double)d2));
     }
+    TPT_STAMP(st, 3);
     float wd = 1.0f;
     // loop A: camera prefix C[0..tl), append L[sl-1], ..., L[0]
     float cur = 1.0f;
@@ -195,14 +201,15 @@ TPT_D V3 path_weight(const DScene& s, const P& paths, int sl, int tl, Packet pk,
         } else {
             const BVert v = k == 0 ? ly : paths.lit(j);
             float pdf;
-            if (k == 0) pdf = append_pdf(s, cz.type, cz.prim, cz.x, cz.N, cpre, v.type, v.x, v.N);
-            else pdf = append_pdf(s, ly.type, ly.prim, ly.x, ly.N, cz.x, v.type, v.x, v.N);
+            if (k == 0) pdf = append_pdf(s, cz.type, cz.mat, cz.x, cz.N, cpre, v.type, v.x, v.N);
+            else pdf = append_pdf(s, ly.type, ly.mat, ly.x, ly.N, cz.x, v.type, v.x, v.N);
             pdf *= rr_of(tl + k);
             cur *= safe_div(pdf, v.pdf);
         }
         wd += cur * cur;
         if (cur == 0.0f) break;
     }
+    TPT_STAMP(st, 4);
     // loop B: light prefix L[0..sl), append C[tl-1], ..., C[0]
     cur = 1.0f;
     for (int k = 0; k < tl; ++k) {
@@ -217,11 +224,11 @@ TPT_D V3 path_weight(const DScene& s, const P& paths, int sl, int tl, Packet pk,
                 pdf = prim_pdf(s, v.prim);  // Append(count==0): vertex.obj->pdf(), no RR factor
             } else {
                 if (k == 0) {
-                    pdf = append_pdf(s, ly.type, ly.prim, ly.x, ly.N, lpre, v.type, v.x, v.N);
+                    pdf = append_pdf(s, ly.type, ly.mat, ly.x, ly.N, lpre, v.type, v.x, v.N);
                 } else {
                     // last = C[tl-1] as appended (type Light when it opened the path, BDPT.cpp:240-242)
                     const int at = sl == 0 ? T_LIGHT : cz.type;
-                    pdf = append_pdf(s, at, cz.prim, cz.x, cz.N, sl >= 1 ? ly.x : cz.x, v.type, v.x, v.N);
+                    pdf = append_pdf(s, at, cz.mat, cz.x, cz.N, sl >= 1 ? ly.x : cz.x, v.type, v.x, v.N);
                 }
                 pdf *= rr_of(count);
             }
@@ -230,6 +237,7 @@ TPT_D V3 path_weight(const DScene& s, const P& paths, int sl, int tl, Packet pk,
         wd += cur * cur;
         if (cur == 0.0f) break;
     }
+    TPT_STAMP(st, 5);
     V3 lt = sl == 0 ? v3s(1.0f) : ly.alpha;
     V3 uc = lt * cz.alpha * cst;
     return divs(uc, wd);
@@ -272,10 +280,11 @@ TPT_D void camera_vertices(const DScene& s, int64_t i, BVert& c0, BVert& c1, int
     const int px = (int)(i % s.width), py = (int)(i / s.width);
     const V3 dir = pixel_ray(px, py, s.width, s.height, s.scale);
     const V3 eye = v3(s.eye[0], s.eye[1], s.eye[2]);
-    c0.x = eye; c0.N = v3s(0.0f); c0.type = T_CAM; c0.prim = -1;
+    c0.x = eye; c0.N = v3s(0.0f); c0.type = T_CAM; c0.prim = -1; c0.mat = -1;
     c0.pdf = kCamZeroPdf; c0.alpha = v3s(1.0f); c0.q1 = c0.q8 = 0.0f;
     PTV h1 = scene_intersect(s, make_ray(eye, dir), TPT_CULL_BACK, stk);
     c1.x = h1.x; c1.N = h1.N; c1.type = h1.type; c1.prim = h1.prim;
+    c1.mat = h1.prim >= 0 ? prim_mat(s, h1.prim) : -1;
     c1.pdf = srpdf_to_area(kCamRayPdf, T_CAM, c0.x, c0.N, h1.type, h1.x, h1.N);
     c1.alpha = v3s(1.0f);
     c1.q1 = c1.q8 = 0.0f;
@@ -296,7 +305,7 @@ TPT_D void generate_paths(const DScene& s, const BVert& c0, const BVert& c1, uin
     int pp;
     object_sample(s, lo, pc, pn, pp, rs);
     BVert l0;
-    l0.x = pc; l0.N = pn; l0.type = T_LIGHT; l0.prim = pp;
+    l0.x = pc; l0.N = pn; l0.type = T_LIGHT; l0.prim = pp; l0.mat = lo.mat;
     l0.pdf = lo.pdf;
     l0.alpha = divs(lem, l0.pdf);
     l0.q1 = l0.q8 = 0.0f;
@@ -308,6 +317,7 @@ TPT_D void generate_paths(const DScene& s, const BVert& c0, const BVert& c1, uin
     PTV it = kPacket ? scene_intersect_packet(s, lr, TPT_CULL_BACK, pk) : scene_intersect(s, lr, TPT_CULL_BACK, stk);
     BVert l1;
     l1.x = it.x; l1.N = it.N; l1.type = it.type; l1.prim = it.prim;
+    l1.mat = it.prim >= 0 ? prim_mat(s, it.prim) : -1;
     l1.pdf = srpdf_to_area(pdf1, T_LIGHT, l0.x, l0.N, it.type, it.x, it.N);
     l1.alpha = v3s(0.0f);  // fresh InternalPathVertex (BDPT.hpp:19)
     l1.q1 = l1.q8 = 0.0f;
@@ -345,7 +355,11 @@ TPT_D void bdpt_pixel(const DScene& s, int64_t i, int spp, V3& acc, float* splat
         const int np = cn * (ln + 1);
         for (int pi = 1; pi < np; ++pi) {
             const int t = pi / (ln + 1) + 1, sl = pi % (ln + 1);
-            V3 w = vmax0(path_weight<PrivPaths, kPacket>(s, paths, sl, t, pk, stk));
+#ifdef TPT_STAMPS
+            Stamps st{};
+            st.last = stamp_now();
+#endif
+            V3 w = vmax0(path_weight<PrivPaths, kPacket>(s, paths, sl, t, pk, stk TPT_STAMPS_PASS));
             if (t > 1) res = res + w;
             else if (splat) splat_add(s, L[sl - 1].x, C[0].x, w, splat);
         }
@@ -364,7 +378,7 @@ TPT_D void bdpt_pixel(const DScene& s, int64_t i, int spp, V3& acc, float* splat
 //            t = 1 splats go straight to the splat buffer;
 //   fold:    per pixel, result += w over its strategies in (t, s) order (t > 1) and
 //            fb += (1/spp) * result -- the reference's summation order.
-// One vertex record = 64 B = four float4: (x, type|prim) (N, pdf) (alpha, -) (q1, q8, -, -),
+// One vertex record = 64 B = four float4: (x, type|prim) (N, pdf) (alpha, mat) (q1, q8, -, -),
 // laid out [pixel][slot] so a vertex is one contiguous line segment (4 x 16-B accesses).
 constexpr int kRecV = 4;  // float4 per vertex record
 struct WfState {
@@ -387,7 +401,7 @@ TPT_D void rec_store(const WfState& w, int slot, int64_t k, const BVert& v) {
     float4* r = rec_at(w.rec, k, slot);
     r[0] = make_float4(v.x.x, v.x.y, v.x.z, __builtin_bit_cast(float, tp_pack(v.type, v.prim)));
     r[1] = make_float4(v.N.x, v.N.y, v.N.z, v.pdf);
-    r[2] = make_float4(v.alpha.x, v.alpha.y, v.alpha.z, 0.0f);
+    r[2] = make_float4(v.alpha.x, v.alpha.y, v.alpha.z, __builtin_bit_cast(float, v.mat));
     r[3] = make_float4(v.q1, v.q8, 0.0f, 0.0f);
 }
 TPT_D void rec_store_q(const WfState& w, int slot, int64_t k, float q1, float q8) {
@@ -407,7 +421,7 @@ TPT_D int fill_path_rec(const DScene& s, const WfState& w, int64_t k, int base, 
     for (int i = start; i < kMaxLen - 1; i++) {
         if (cur.type == T_BG) break;
         V3 wo = normalized(prev.x - cur.x);
-        const Mat m = load_mat(s, prim_mat(s, cur.prim));
+        const Mat m = load_mat(s, cur.mat);
         float raw;
         V3 wi = mat_sample(m, wo, cur.N, &raw, rs);
         const float rr = i > 4 ? .8f : 1.f;
@@ -422,13 +436,14 @@ TPT_D int fill_path_rec(const DScene& s, const WfState& w, int64_t k, int base, 
         V3 bsdf = eval_bsdf(m, wo, wi, cur.N, false);
         BVert nx;
         nx.x = it.x; nx.N = it.N; nx.type = it.type; nx.prim = it.prim;
+        nx.mat = it.prim >= 0 ? prim_mat(s, it.prim) : -1;
         nx.pdf = pdf * rr;
         nx.alpha = divs(cur.alpha * safe_div(bsdf, sr), rr);
         nx.q1 = nx.q8 = 0.0f;
         rec_store(w, base + i + 1, k, nx);
         count++;
         // path_rev for j = i - 1: Append(P[j]) after last = P[i], Pre = P[i+1]
-        const float rev = append_pdf(s, cur.type, cur.prim, cur.x, cur.N, nx.x, prev.type, prev.x, prev.N);
+        const float rev = append_pdf(s, cur.type, cur.mat, cur.x, cur.N, nx.x, prev.type, prev.x, prev.N);
         rec_store_q(w, base + i - 1, k, safe_div(rev * 1.f, prev.pdf), safe_div(rev * .8f, prev.pdf));
         prev = cur;
         cur = nx;
@@ -450,6 +465,7 @@ struct GlobPaths {  // one pixel's paths in the HBM records
         v.N = v3(b.x, b.y, b.z);
         v.pdf = b.w;
         v.alpha = v3(c.x, c.y, c.z);
+        v.mat = __builtin_bit_cast(int, c.w);
         v.q1 = q.x;
         v.q8 = q.y;
         return v;

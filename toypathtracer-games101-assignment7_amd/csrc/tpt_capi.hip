@@ -35,7 +35,7 @@ extern __shared__ __align__(16) unsigned char tpt_smem[];
     pk.node = pk_node[threadIdx.x / 64];                                  \
     pk.mask = pk_mask[threadIdx.x / 64];
 
-// Workgroup prologue: LDS = [traversal stack: max_stack x kBlock ints][nodes][tris][qnodes].
+// Workgroup prologue: LDS = [traversal stack: max_stack x kBlock ints][nodes][tris][qnodes][mats].
 // With kLds the scene's node and triangle arrays are copied into LDS (16 B per lane
 // per step) and the kernel's DScene is pointed at them, so every traversal fetch is
 // a ds_read instead of a dependent L1/L2 load.
@@ -45,7 +45,7 @@ TPT_D int* stage_scene(DScene& s) {
     if (kLds) {
         unsigned char* base = tpt_smem + (size_t)s.max_stack * kBlock * sizeof(int);
         const int nb = s.nnodes * (int)sizeof(DNode), tb = s.ntri * (int)sizeof(DTri),
-                  qb = s.nqnodes * (int)sizeof(DQNode);
+                  qb = s.nqnodes * (int)sizeof(DQNode), mb = s.nmats * (int)sizeof(DMat);
         const uint4* gn = reinterpret_cast<const uint4*>(s.nodes);
         const uint4* gt = reinterpret_cast<const uint4*>(s.tris);
         const uint4* gq = reinterpret_cast<const uint4*>(s.qnodes);
@@ -55,10 +55,14 @@ TPT_D int* stage_scene(DScene& s) {
         for (int i = threadIdx.x; i < nb / 16; i += kBlock) ln[i] = gn[i];
         for (int i = threadIdx.x; i < tb / 16; i += kBlock) lt[i] = gt[i];
         for (int i = threadIdx.x; i < qb / 16; i += kBlock) lq[i] = gq[i];
+        const uint4* gm = reinterpret_cast<const uint4*>(s.mats);
+        uint4* lm = reinterpret_cast<uint4*>(base + nb + tb + qb);
+        for (int i = threadIdx.x; i < (mb + 15) / 16; i += kBlock) lm[i] = gm[i];  // 72-B records: round up
         __syncthreads();
         s.nodes = reinterpret_cast<const DNode*>(base);
         s.tris = reinterpret_cast<const DTri*>(base + nb);
         s.qnodes = reinterpret_cast<const DQNode*>(base + nb + tb);
+        s.mats = reinterpret_cast<const DMat*>(base + nb + tb + qb);
     }
     return stk;
 }
@@ -213,7 +217,7 @@ __global__ __launch_bounds__(kBlock, TPT_GEN_MINWAVES) void tpt_bdpt_gen_kernel(
     int pp;
     object_sample(s, lo, pc, pn, pp, rs);
     BVert l0;
-    l0.x = pc; l0.N = pn; l0.type = T_LIGHT; l0.prim = pp;
+    l0.x = pc; l0.N = pn; l0.type = T_LIGHT; l0.prim = pp; l0.mat = lo.mat;
     l0.pdf = lo.pdf;
     l0.alpha = divs(load_mat(s, lo.mat).em, l0.pdf);
     l0.q1 = l0.q8 = 0.0f;
@@ -224,6 +228,7 @@ __global__ __launch_bounds__(kBlock, TPT_GEN_MINWAVES) void tpt_bdpt_gen_kernel(
     PTV it = scene_intersect(s, make_ray(l0.x, wi), TPT_CULL_BACK, stk);
     BVert l1;
     l1.x = it.x; l1.N = it.N; l1.type = it.type; l1.prim = it.prim;
+    l1.mat = it.prim >= 0 ? prim_mat(s, it.prim) : -1;
     l1.pdf = srpdf_to_area(pdf1, T_LIGHT, l0.x, l0.N, it.type, it.x, it.N);
     l1.alpha = v3s(0.0f);  // fresh InternalPathVertex (BDPT.hpp:19)
     l1.q1 = l1.q8 = 0.0f;
@@ -255,13 +260,19 @@ __global__ __launch_bounds__(kBlock, TPT_CONN_MINWAVES) void tpt_bdpt_conn_kerne
     TPT_PACKET_DECL
     const int64_t total = w.incl[w.n - 1];
     const V3 eye = v3(s.eye[0], s.eye[1], s.eye[2]);
+#ifdef TPT_STAMPS
+    Stamps st{};
+    st.last = stamp_now();
+#endif
     for (int64_t g = (int64_t)blockIdx.x * kBlock + threadIdx.x; g < total; g += (int64_t)gridDim.x * kBlock) {
+        TPT_STAMP(st, 0);
         const unsigned long long tk = w.task[g];
         const int64_t k = (int64_t)(tk & 0xffffffffffull);
         const int t = (int)((tk >> 40) & 0xff), sl = (int)(tk >> 48);
         GlobPaths P;
         P.rec = rec_at(w.rec, k, 0);
-        const V3 v = vmax0(path_weight<GlobPaths, false>(s, P, sl, t, pk, stk));
+        const V3 v = vmax0(path_weight<GlobPaths, false>(s, P, sl, t, pk, stk TPT_STAMPS_PASS));
+        TPT_STAMP(st, 6);
         if (t > 1) {
             w.res[3 * g] = v.x;
             w.res[3 * g + 1] = v.y;
@@ -269,7 +280,13 @@ __global__ __launch_bounds__(kBlock, TPT_CONN_MINWAVES) void tpt_bdpt_conn_kerne
         } else if (splat) {
             splat_add(s, P.lit(sl - 1).x, eye, v, splat);
         }
+        TPT_STAMP(st, 7);
     }
+#ifdef TPT_STAMPS
+    TPT_STAMP(st, 0);
+    if (lane_id() == 0)
+        for (int x = 0; x < 12; ++x) atomicAdd(s.dbgc + 8 + x, st.acc[x]);
+#endif
 }
 
 __global__ __launch_bounds__(kBlock) void tpt_bdpt_fold_kernel(WfState w, float inv) {
@@ -547,6 +564,14 @@ int launch(tpt_ctx* c, int mode, int spp, int64_t begin, int64_t stride, int64_t
                      (double)d[5] / d[7], (double)d[6] / d[7]);
     }
 #ifdef TPT_STAMPS
+    if (mode == TPT_MODE_BDPT) {
+        unsigned long long d[12];
+        HIP_TRY(c, hipMemcpy(d, c->counters + 16, sizeof(d), hipMemcpyDeviceToHost));
+        static const char* nm[8] = {"loop/decode", "loads", "shadow", "eval x2", "loop A", "loop B", "tail", "store/splat"};
+        double tot = 0;
+        for (int x = 0; x < 8; ++x) tot += (double)d[x];
+        for (int x = 0; x < 8; ++x) std::fprintf(stderr, "[tpt stamps] conn %-12s %5.1f%%\n", nm[x], 100.0 * d[x] / tot);
+    }
     if (mode == TPT_MODE_PT) {
         unsigned long long d[12];
         HIP_TRY(c, hipMemcpy(d, c->counters + 16, sizeof(d), hipMemcpyDeviceToHost));
@@ -667,6 +692,7 @@ int tpt_upload_scene(tpt_ctx* c, const tpt_scene_desc* d) {
     ds.emitters = (const int32_t*)(b + o_em);
     ds.qnodes = (const DQNode*)(b + o_q);
     ds.nqnodes = (int)hs.qnodes.size();
+    ds.nmats = (int)hs.mats.size();
     ds.n_emitters = (int)hs.emitters.size();
     // BVHAccel::Sample (1 draw) + Triangle::Sample (2) per mesh emitter, Sphere::Sample (2)
     ds.light_draws = 0;
@@ -685,7 +711,7 @@ int tpt_upload_scene(tpt_ctx* c, const tpt_scene_desc* d) {
     // Cornell presets need ~6 KB).
     {
         const size_t sb = hs.nodes.size() * sizeof(DNode) + hs.tris.size() * sizeof(DTri) +
-                          hs.qnodes.size() * sizeof(DQNode);
+                          ((hs.mats.size() * sizeof(DMat) + 15) & ~(size_t)15) + hs.qnodes.size() * sizeof(DQNode);
         const char* no = std::getenv("TPT_NO_LDS");
         ds.lds_bytes = (sb <= 64 * 1024 && !(no && no[0] == '1')) ? (int)sb : 0;
         const char* dbg = std::getenv("TPT_DEBUG_FLAGS");

@@ -107,6 +107,7 @@ struct DScene {
     float eye[3];
     float bg[3];
     int32_t nqnodes;
+    int32_t nmats;
     int32_t max_stack;  // LDS stack entries per lane a binary-tree walk can need (depth + 1)
     int32_t q_stack;    // ... and a per-lane walk of the 4-wide shadow tree (3 per level + 1)
     int32_t lds_bytes;  // bytes of nodes + triangles + qnodes staged in LDS per workgroup (0 = read from HBM/L2)
