@@ -371,8 +371,10 @@ TPT_D void bdpt_pixel(const DScene& s, int64_t i, int spp, V3& acc, float* splat
 // Per sample iteration, for every pixel of the shard:
 //   gen:     generate both subpaths (RNG-sequential per pixel) and write them to
 //            HBM as SoA records [path*16+vertex][field][pixel];
-//   scan:    inclusive prefix sum of the strategy counts cn*(ln+1)-1;
-//   scatter: task[g] = (pixel, t, s) for every strategy g;
+//   scan:    inclusive prefix sums of the strategy counts (s = 0 ones and the others);
+//   scatter: task[g] = (pixel, t, s) for every strategy, the s = 0 (emission-only)
+//            strategies first and the connecting ones after, so a wave holds one
+//            kind; tres[g] = the strategy's canonical (t, s)-order slot;
 //   connect: ONE LANE PER STRATEGY (PathWeight), so a wave's work is 64 strategies
 //            instead of the longest lane's cn*(ln+1) (measured 18 mean vs 73 max);
 //            t = 1 splats go straight to the splat buffer;
@@ -384,8 +386,9 @@ constexpr int kRecV = 4;  // float4 per vertex record
 struct WfState {
     float4* rec;          // n * 32 * kRecV float4
     int* cnt;             // cn | ln << 16
-    int* np;              // strategies per pixel
-    int* incl;            // inclusive scan of np
+    unsigned long long* np;    // strategies per pixel: (s = 0 ones: cn - 1) | (the others: cn * ln) << 32
+    unsigned long long* incl;  // inclusive scan of np (both halves at once)
+    int* tres;            // task -> canonical strategy index (res slot)
     unsigned long long* task;  // strategy -> pixel | t << 40 | s << 48
     float* res;           // 3 floats per strategy
     uint32_t* rng;        // XorShift state per pixel stream

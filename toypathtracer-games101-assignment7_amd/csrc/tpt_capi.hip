@@ -238,19 +238,39 @@ __global__ __launch_bounds__(kBlock, TPT_GEN_MINWAVES) void tpt_bdpt_gen_kernel(
     const int ln = (pdf1 == 0.0f && it.type == T_BG) ? 2 : fill_path_rec<false>(s, w, k, kMaxLen, l0, l1, 1, rs, pk, stk);
     w.rng[k] = rs;
     w.cnt[k] = cn | (ln << 16);
-    w.np[k] = cn * (ln + 1) - 1;
+    w.np[k] = (unsigned long long)(cn - 1) | ((unsigned long long)(cn * ln) << 32);
     atomicAdd(w.bounces, (unsigned long long)(cn + ln));
+}
+
+// Canonical (t, s)-order range of pixel k's strategies and the starts of its two
+// task runs (s = 0 run in [0, n0_total), connecting run after it).
+struct StratRange {
+    int64_t canon, b0, b1;
+    int n0, n1, ln;
+};
+TPT_D StratRange strat_range(const WfState& w, int64_t k) {
+    const unsigned long long e = w.incl[k], c = w.np[k];
+    StratRange r;
+    r.n0 = (int)(c & 0xffffffffull);
+    r.n1 = (int)(c >> 32);
+    r.b0 = (int64_t)(e & 0xffffffffull) - r.n0;
+    r.b1 = (int64_t)(e >> 32) - r.n1;
+    r.canon = r.b0 + r.b1;
+    r.ln = w.cnt[k] >> 16;
+    return r;
 }
 
 __global__ __launch_bounds__(kBlock) void tpt_bdpt_scatter_kernel(WfState w) {
     const int64_t k = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (k >= w.n) return;
-    const int e = w.incl[k], b = e - w.np[k];
-    const int ln = w.cnt[k] >> 16;
-    for (int g = b; g < e; ++g) {
-        const int pi = g - b + 1;  // strategy index in (t, s) order; pi = 0 skipped
-        const unsigned long long t = (unsigned long long)(pi / (ln + 1) + 1), sl = (unsigned long long)(pi % (ln + 1));
-        w.task[g] = (unsigned long long)k | (t << 40) | (sl << 48);
+    const StratRange r = strat_range(w, k);
+    const int64_t n0_total = (int64_t)(w.incl[w.n - 1] & 0xffffffffull);
+    const int np = r.n0 + r.n1;
+    for (int pi = 1; pi <= np; ++pi) {  // strategy index in (t, s) order; pi = 0 skipped
+        const int t = pi / (r.ln + 1) + 1, sl = pi % (r.ln + 1);
+        const int64_t g = sl == 0 ? r.b0 + (t - 2) : n0_total + r.b1 + (int64_t)(t - 1) * r.ln + (sl - 1);
+        w.task[g] = (unsigned long long)k | ((unsigned long long)t << 40) | ((unsigned long long)sl << 48);
+        w.tres[g] = (int)(r.canon + pi - 1);
     }
 }
 
@@ -258,7 +278,8 @@ template <bool kLds>
 __global__ __launch_bounds__(kBlock, TPT_CONN_MINWAVES) void tpt_bdpt_conn_kernel(DScene s, WfState w, float* __restrict__ splat) {
     int* stk = stage_scene<kLds>(s);
     TPT_PACKET_DECL
-    const int64_t total = w.incl[w.n - 1];
+    const unsigned long long tot = w.incl[w.n - 1];
+    const int64_t total = (int64_t)(tot & 0xffffffffull) + (int64_t)(tot >> 32);
     const V3 eye = v3(s.eye[0], s.eye[1], s.eye[2]);
 #ifdef TPT_STAMPS
     Stamps st{};
@@ -274,9 +295,10 @@ __global__ __launch_bounds__(kBlock, TPT_CONN_MINWAVES) void tpt_bdpt_conn_kerne
         const V3 v = vmax0(path_weight<GlobPaths, false>(s, P, sl, t, pk, stk TPT_STAMPS_PASS));
         TPT_STAMP(st, 6);
         if (t > 1) {
-            w.res[3 * g] = v.x;
-            w.res[3 * g + 1] = v.y;
-            w.res[3 * g + 2] = v.z;
+            const int64_t ri = w.tres[g];
+            w.res[3 * ri] = v.x;
+            w.res[3 * ri + 1] = v.y;
+            w.res[3 * ri + 2] = v.z;
         } else if (splat) {
             splat_add(s, P.lit(sl - 1).x, eye, v, splat);
         }
@@ -292,13 +314,12 @@ __global__ __launch_bounds__(kBlock, TPT_CONN_MINWAVES) void tpt_bdpt_conn_kerne
 __global__ __launch_bounds__(kBlock) void tpt_bdpt_fold_kernel(WfState w, float inv) {
     const int64_t k = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (k >= w.n) return;
-    const int e = w.incl[k], b = e - w.np[k];
-    const int ln = w.cnt[k] >> 16;
+    const StratRange r = strat_range(w, k);
+    const int64_t b = r.canon, e = r.canon + r.n0 + r.n1;
+    const int ln = r.ln;
     V3 res = v3s(0.0f);  // BDPT.cpp:289 `Vector3f result;`
-    for (int g = b; g < e; ++g) {
-        const int pi = g - b + 1;
-        if (pi / (ln + 1) + 1 > 1) res = res + v3(w.res[3 * g], w.res[3 * g + 1], w.res[3 * g + 2]);
-    }
+    for (int64_t g = b + ln; g < e; ++g)  // pi = g - b + 1 > ln: t > 1 (t = 1 strategies were splatted)
+        res = res + v3(w.res[3 * g], w.res[3 * g + 1], w.res[3 * g + 2]);
     V3 acc = v3(w.acc[3 * k], w.acc[3 * k + 1], w.acc[3 * k + 2]);
     acc = acc + mul(res, inv);  // Renderer.cpp:49 `fb[i] += (1.0f / spp) * BDPT(...)`
     w.acc[3 * k] = acc.x;
@@ -416,9 +437,9 @@ int ensure_wf(tpt_ctx* c, int64_t n) {
     c->wf_cap = 0;
     const int64_t maxs = (int64_t)kMaxLen * (kMaxLen + 1) - 1;
     auto al = [](int64_t b) { return (b + 255) & ~(int64_t)255; };
-    const int64_t b_rec = al(2 * kMaxLen * kRecV * n * 16), b_i = al(n * 4), b_own = al(n * maxs * 8),
-                  b_res = al(n * maxs * 12), b_acc = al(n * 12);
-    const int64_t per_buf = b_rec + 3 * b_i + b_own + b_res;
+    const int64_t b_rec = al(2 * kMaxLen * kRecV * n * 16), b_i = al(n * 4), b_l = al(n * 8),
+                  b_own = al(n * maxs * 8), b_tres = al(n * maxs * 4), b_res = al(n * maxs * 12), b_acc = al(n * 12);
+    const int64_t per_buf = b_rec + b_i + 2 * b_l + b_own + b_tres + b_res;
     const int64_t total = 2 * per_buf + b_i + b_acc;
     HIP_TRY(c, hipMalloc(&c->wf_mem, total));
     char* p = (char*)c->wf_mem;
@@ -426,16 +447,18 @@ int ensure_wf(tpt_ctx* c, int64_t n) {
         WfState& w = c->wf[b];
         w.rec = (float4*)p; p += b_rec;
         w.cnt = (int*)p; p += b_i;
-        w.np = (int*)p; p += b_i;
-        w.incl = (int*)p; p += b_i;
+        w.np = (unsigned long long*)p; p += b_l;
+        w.incl = (unsigned long long*)p; p += b_l;
         w.task = (unsigned long long*)p; p += b_own;
+        w.tres = (int*)p; p += b_tres;
         w.res = (float*)p; p += b_res;
     }
     c->wf[0].rng = c->wf[1].rng = (uint32_t*)p; p += b_i;
     c->wf[0].acc = c->wf[1].acc = (float*)p;
     const WfState& w = c->wf[0];
     size_t bytes = 0;
-    HIP_TRY(c, rocprim::inclusive_scan(nullptr, bytes, w.np, w.incl, (size_t)n, rocprim::plus<int>(), c->stream));
+    HIP_TRY(c, rocprim::inclusive_scan(nullptr, bytes, w.np, w.incl, (size_t)n, rocprim::plus<unsigned long long>(),
+                                       c->stream));
     HIP_TRY(c, hipMalloc(&c->scan_tmp, bytes));
     c->scan_bytes = bytes;
     c->wf_cap = n;
@@ -499,7 +522,8 @@ int launch(tpt_ctx* c, int mode, int spp, int64_t begin, int64_t stride, int64_t
                 hipLaunchKernelGGL(tpt_bdpt_gen_kernel<false>, dim3(pblocks), dim3(kBlock), shmem, c->stream, c->ds, w,
                                    it == 0 ? 1 : 0);
             size_t bytes = c->scan_bytes;
-            HIP_TRY(c, rocprim::inclusive_scan(c->scan_tmp, bytes, w.np, w.incl, (size_t)count, rocprim::plus<int>(),
+            HIP_TRY(c, rocprim::inclusive_scan(c->scan_tmp, bytes, w.np, w.incl, (size_t)count,
+                                               rocprim::plus<unsigned long long>(),
                                                c->stream));
             hipLaunchKernelGGL(tpt_bdpt_scatter_kernel, dim3(pblocks), dim3(kBlock), 0, c->stream, w);
             HIP_TRY(c, hipEventRecord(c->ev_gen[b], c->stream));
