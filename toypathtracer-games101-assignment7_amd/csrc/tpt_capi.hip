@@ -197,19 +197,30 @@ __global__ __launch_bounds__(kBlock) void tpt_bdpt_kernel(DScene s, int spp, int
 #endif
 
 template <bool kLds>
-__global__ __launch_bounds__(kBlock, TPT_GEN_MINWAVES) void tpt_bdpt_gen_kernel(DScene s, WfState w, int first) {
+__global__ __launch_bounds__(kBlock, TPT_GEN_MINWAVES) void tpt_bdpt_gen_kernel(DScene s, WfState w, int iter) {
     int* stk = stage_scene<kLds>(s);
     TPT_PACKET_DECL
     const int64_t k = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (k >= w.n) return;
     const int64_t i = wf_pixel(w, k);
+    const bool first = iter == 0;
     BVert c0, c1;
-    camera_vertices(s, i, c0, c1, stk);
+    if (iter >= 2) {
+        // GenerateCameraPath's v0/v1 do not depend on the sample (no jitter): this
+        // buffer's slots 0/1 still hold them from iteration iter - 2 (their q1/q8 may
+        // be stale, but those of vertices cn-2 and cn-1 are never read).
+        GlobPaths P;
+        P.rec = rec_at(w.rec, k, 0);
+        c0 = P.cam(0);
+        c1 = P.cam(1);
+    } else {
+        camera_vertices(s, i, c0, c1, stk);
+        rec_store(w, 0, k, c0);
+        rec_store(w, 1, k, c1);
+    }
     uint32_t rs = first ? (uint32_t)((int)i + 1) : w.rng[k];  // ResetRandom(i + 1), Renderer.cpp:42
     if (first) { w.acc[3 * k] = 0.0f; w.acc[3 * k + 1] = 0.0f; w.acc[3 * k + 2] = 0.0f; }
     // generate_paths (tpt_bdpt.h) with the vertices streamed into the records
-    rec_store(w, 0, k, c0);
-    rec_store(w, 1, k, c1);
     const int cn = fill_path_rec<false>(s, w, k, 0, c0, c1, 1, rs, pk, stk);
     // GenerateLightPath (BDPT.cpp:61-90) from m_emissionObjects[0]
     const DObj lo = s.objs[s.emitters[0]];
@@ -516,11 +527,9 @@ int launch(tpt_ctx* c, int mode, int spp, int64_t begin, int64_t stride, int64_t
             w.bounces = c->counters;
             if (it >= 2) HIP_TRY(c, hipStreamWaitEvent(c->stream, c->ev_fold[b], 0));
             if (lds)
-                hipLaunchKernelGGL(tpt_bdpt_gen_kernel<true>, dim3(pblocks), dim3(kBlock), shmem, c->stream, c->ds, w,
-                                   it == 0 ? 1 : 0);
+                hipLaunchKernelGGL(tpt_bdpt_gen_kernel<true>, dim3(pblocks), dim3(kBlock), shmem, c->stream, c->ds, w, it);
             else
-                hipLaunchKernelGGL(tpt_bdpt_gen_kernel<false>, dim3(pblocks), dim3(kBlock), shmem, c->stream, c->ds, w,
-                                   it == 0 ? 1 : 0);
+                hipLaunchKernelGGL(tpt_bdpt_gen_kernel<false>, dim3(pblocks), dim3(kBlock), shmem, c->stream, c->ds, w, it);
             size_t bytes = c->scan_bytes;
             HIP_TRY(c, rocprim::inclusive_scan(c->scan_tmp, bytes, w.np, w.incl, (size_t)count,
                                                rocprim::plus<unsigned long long>(),
