@@ -411,47 +411,74 @@ TPT_D void rec_store_q(const WfState& w, int slot, int64_t k, float q1, float q8
     *reinterpret_cast<float2*>(rec_at(w.rec, k, slot) + 3) = make_float2(q1, q8);
 }
 
-// fill_path + path_rev streamed into the HBM records (slots base+start+1, ...):
-// the same vertices, draws and float ops, but only a window of three vertices is
-// live.  Vertex j's reverse pdf needs P[j], P[j+1] and P[j+2].x, so it is computed
-// as soon as P[j+2] has been appended -- the private 2 x 16-vertex arrays (1.8 KB
-// of scratch per lane) are gone.  `prev` = P[start-1], `cur` = P[start], both
-// already stored.
+// fill_path + path_rev streamed into the HBM records, one vertex per call: the
+// body of FillPathUsingRussianRoulette's loop (BDPT.cpp:92-118) for the subpath at
+// slots base.. whose last two vertices are prev = P[i-1] and cur = P[i].  Same
+// vertices, draws and float ops as fill_path + path_rev; vertex j's reverse pdf
+// needs P[j], P[j+1] and P[j+2].x, so it is computed as soon as P[j+2] exists and
+// only a three-vertex window is live.  Returns false when the subpath has ended
+// (its vertex count is then i + 1).
 template <bool kPacket>
-TPT_D int fill_path_rec(const DScene& s, const WfState& w, int64_t k, int base, BVert prev, BVert cur, int start,
-                        uint32_t& rs, Packet pk, int* stk) {
-    int count = start + 1;
-    for (int i = start; i < kMaxLen - 1; i++) {
-        if (cur.type == T_BG) break;
-        V3 wo = normalized(prev.x - cur.x);
-        const Mat m = load_mat(s, cur.mat);
-        float raw;
-        V3 wi = mat_sample(m, wo, cur.N, &raw, rs);
-        const float rr = i > 4 ? .8f : 1.f;
-        if (rng_float(rs) > rr) break;
-        float ct = (float)dabs_(dot3(cur.N, wi));
-        float sr = safe_div(raw, ct);
-        const Ray nr = make_ray(cur.x, wi);
-        const int cl = dot3(cur.N, wi) > 0.0f ? TPT_CULL_BACK : TPT_CULL_FRONT;
-        PTV it = kPacket ? scene_intersect_packet(s, nr, cl, pk) : scene_intersect(s, nr, cl, stk);
-        float pdf = srpdf_to_area(sr, cur.type, cur.x, cur.N, it.type, it.x, it.N);
-        if (pdf == 0.0f) break;
-        V3 bsdf = eval_bsdf(m, wo, wi, cur.N, false);
-        BVert nx;
-        nx.x = it.x; nx.N = it.N; nx.type = it.type; nx.prim = it.prim;
-        nx.mat = it.prim >= 0 ? prim_mat(s, it.prim) : -1;
-        nx.pdf = pdf * rr;
-        nx.alpha = divs(cur.alpha * safe_div(bsdf, sr), rr);
-        nx.q1 = nx.q8 = 0.0f;
-        rec_store(w, base + i + 1, k, nx);
-        count++;
-        // path_rev for j = i - 1: Append(P[j]) after last = P[i], Pre = P[i+1]
-        const float rev = append_pdf(s, cur.type, cur.mat, cur.x, cur.N, nx.x, prev.type, prev.x, prev.N);
-        rec_store_q(w, base + i - 1, k, safe_div(rev * 1.f, prev.pdf), safe_div(rev * .8f, prev.pdf));
-        prev = cur;
-        cur = nx;
-    }
-    return count;
+TPT_D bool extend_rec(const DScene& s, const WfState& w, int64_t k, int base, BVert& prev, BVert& cur, int& i,
+                      uint32_t& rs, Packet pk, int* stk) {
+    if (i >= kMaxLen - 1 || cur.type == T_BG) return false;
+    V3 wo = normalized(prev.x - cur.x);
+    const Mat m = load_mat(s, cur.mat);
+    float raw;
+    V3 wi = mat_sample(m, wo, cur.N, &raw, rs);
+    const float rr = i > 4 ? .8f : 1.f;
+    if (rng_float(rs) > rr) return false;
+    float ct = (float)dabs_(dot3(cur.N, wi));
+    float sr = safe_div(raw, ct);
+    const Ray nr = make_ray(cur.x, wi);
+    const int cl = dot3(cur.N, wi) > 0.0f ? TPT_CULL_BACK : TPT_CULL_FRONT;
+    PTV it = kPacket ? scene_intersect_packet(s, nr, cl, pk) : scene_intersect(s, nr, cl, stk);
+    float pdf = srpdf_to_area(sr, cur.type, cur.x, cur.N, it.type, it.x, it.N);
+    if (pdf == 0.0f) return false;
+    V3 bsdf = eval_bsdf(m, wo, wi, cur.N, false);
+    BVert nx;
+    nx.x = it.x; nx.N = it.N; nx.type = it.type; nx.prim = it.prim;
+    nx.mat = it.prim >= 0 ? prim_mat(s, it.prim) : -1;
+    nx.pdf = pdf * rr;
+    nx.alpha = divs(cur.alpha * safe_div(bsdf, sr), rr);
+    nx.q1 = nx.q8 = 0.0f;
+    rec_store(w, base + i + 1, k, nx);
+    // path_rev for j = i - 1: Append(P[j]) after last = P[i], Pre = P[i+1]
+    const float rev = append_pdf(s, cur.type, cur.mat, cur.x, cur.N, nx.x, prev.type, prev.x, prev.N);
+    rec_store_q(w, base + i - 1, k, safe_div(rev * 1.f, prev.pdf), safe_div(rev * .8f, prev.pdf));
+    prev = cur;
+    cur = nx;
+    ++i;
+    return true;
+}
+
+// GenerateLightPath's first two vertices (BDPT.cpp:61-90, m_emissionObjects[0]),
+// stored at slots kMaxLen, kMaxLen + 1.  Returns false when the path ends there
+// (pdf1 == 0 and the ray escaped: ln = 2).
+TPT_D bool light_start_rec(const DScene& s, const WfState& w, int64_t k, BVert& l0, BVert& l1, uint32_t& rs,
+                           int* stk) {
+    const DObj lo = s.objs[s.emitters[0]];
+    V3 pc, pn;
+    int pp;
+    object_sample(s, lo, pc, pn, pp, rs);
+    l0.x = pc; l0.N = pn; l0.type = T_LIGHT; l0.prim = pp; l0.mat = lo.mat;
+    l0.pdf = lo.pdf;
+    l0.alpha = divs(load_mat(s, lo.mat).em, l0.pdf);
+    l0.q1 = l0.q8 = 0.0f;
+    float pdf1;
+    V3 wi = cosine_sample(pn, pdf1, rs);
+    float ct = (float)dot3(l0.N, wi);
+    pdf1 = safe_div(pdf1, ct);
+    PTV it = scene_intersect(s, make_ray(l0.x, wi), TPT_CULL_BACK, stk);
+    l1.x = it.x; l1.N = it.N; l1.type = it.type; l1.prim = it.prim;
+    l1.mat = it.prim >= 0 ? prim_mat(s, it.prim) : -1;
+    l1.pdf = srpdf_to_area(pdf1, T_LIGHT, l0.x, l0.N, it.type, it.x, it.N);
+    l1.alpha = v3s(0.0f);  // fresh InternalPathVertex (BDPT.hpp:19)
+    l1.q1 = l1.q8 = 0.0f;
+    if (pdf1 != 0.0f) l1.alpha = safe_div(l0.alpha, pdf1);
+    rec_store(w, kMaxLen, k, l0);
+    rec_store(w, kMaxLen + 1, k, l1);
+    return !(pdf1 == 0.0f && it.type == T_BG);
 }
 
 struct GlobPaths {  // one pixel's paths in the HBM records

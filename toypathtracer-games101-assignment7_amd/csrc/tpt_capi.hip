@@ -196,62 +196,100 @@ __global__ __launch_bounds__(kBlock) void tpt_bdpt_kernel(DScene s, int spp, int
 #define TPT_CONN_MINWAVES 4  // waves per SIMD (measured: 4 beats 2, 3 and 5)
 #endif
 
+// Path generation, persistent: each lane runs a pixel's sample as a sequence of
+// steps (start, camera-path vertex..., light start, light-path vertex...) and takes
+// the next pixel from its shard's queue as soon as it is done, so a wave stays full
+// although path lengths differ per lane (a lane-per-pixel grid ran at 44 % lane
+// efficiency).  Per-pixel order -- and so every RNG draw -- is unchanged.  Queues:
+// one counter per shard of pixels, shard = blockIdx.x % 8 (blocks b and b + 8 are
+// dealt to the same XCD; speed only).
 template <bool kLds>
-__global__ __launch_bounds__(kBlock, TPT_GEN_MINWAVES) void tpt_bdpt_gen_kernel(DScene s, WfState w, int iter) {
+__global__ __launch_bounds__(kBlock, TPT_GEN_MINWAVES) void tpt_bdpt_gen_kernel(DScene s, WfState w, int iter,
+                                                                               unsigned* __restrict__ queue) {
     int* stk = stage_scene<kLds>(s);
     TPT_PACKET_DECL
-    const int64_t k = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (k >= w.n) return;
-    const int64_t i = wf_pixel(w, k);
-    const bool first = iter == 0;
-    BVert c0, c1;
-    if (iter >= 2) {
-        // GenerateCameraPath's v0/v1 do not depend on the sample (no jitter): this
-        // buffer's slots 0/1 still hold them from iteration iter - 2 (their q1/q8 may
-        // be stale, but those of vertices cn-2 and cn-1 are never read).
-        GlobPaths P;
-        P.rec = rec_at(w.rec, k, 0);
-        c0 = P.cam(0);
-        c1 = P.cam(1);
-    } else {
-        camera_vertices(s, i, c0, c1, stk);
-        rec_store(w, 0, k, c0);
-        rec_store(w, 1, k, c1);
+    const int shard = blockIdx.x & 7;
+    const int64_t k_lo = w.n * shard / 8, k_hi = w.n * (shard + 1) / 8;
+    unsigned* q = queue + shard * 16;  // 64 B apart
+    int64_t k = -1;   // this lane's pixel ordinal (-1: none)
+    int phase = 0;    // 0: camera path, 1: light start pending, 2: light path
+    int i = 0, cn = 0;
+    uint32_t rs = 0;
+    unsigned long long nbounce = 0;
+    bool drained = false;
+    BVert prev, cur;
+    for (;;) {
+        const bool need = k < 0 && !drained;
+        const unsigned long long nm = __ballot(need);
+        if (nm != 0) {
+            const int leader = __builtin_ctzll(nm);
+            unsigned base = 0;
+            if (lane_id() == leader) base = atomicAdd(q, (unsigned)__popcll(nm));
+            base = __shfl(base, leader);
+            if (need) {
+                const int64_t kk = k_lo + base + __popcll(nm & ((1ull << lane_id()) - 1));
+                if (kk < k_hi) {
+                    k = kk;
+                    const int64_t pix = wf_pixel(w, k);
+                    BVert c0, c1;
+                    if (iter >= 2) {
+                        // GenerateCameraPath's v0/v1 do not depend on the sample (no
+                        // jitter): this buffer's slots 0/1 still hold them from iteration
+                        // iter - 2 (their q1/q8 may be stale; those of vertices cn-2,
+                        // cn-1 are never read).
+                        GlobPaths P;
+                        P.rec = rec_at(w.rec, k, 0);
+                        c0 = P.cam(0);
+                        c1 = P.cam(1);
+                    } else {
+                        camera_vertices(s, pix, c0, c1, stk);
+                        rec_store(w, 0, k, c0);
+                        rec_store(w, 1, k, c1);
+                    }
+                    rs = iter == 0 ? (uint32_t)((int)pix + 1) : w.rng[k];  // ResetRandom(i + 1), Renderer.cpp:42
+                    if (iter == 0) { w.acc[3 * k] = 0.0f; w.acc[3 * k + 1] = 0.0f; w.acc[3 * k + 2] = 0.0f; }
+                    prev = c0;
+                    cur = c1;
+                    i = 1;
+                    phase = 0;
+                } else {
+                    drained = true;
+                }
+            }
+        }
+        if (__ballot(k >= 0) == 0) break;  // every lane idle and its shard drained
+        if (k < 0) continue;
+        int ln = -1;  // >= 0: the pixel's sample is complete
+        if (phase == 1) {
+            BVert l0, l1;
+            if (light_start_rec(s, w, k, l0, l1, rs, stk)) {
+                prev = l0;
+                cur = l1;
+                i = 1;
+                phase = 2;
+            } else {
+                ln = 2;
+            }
+        }
+        if (ln < 0 && !extend_rec<false>(s, w, k, phase == 0 ? 0 : kMaxLen, prev, cur, i, rs, pk, stk)) {
+            if (phase == 0) {
+                cn = i + 1;
+                phase = 1;
+            } else {
+                ln = i + 1;
+            }
+        }
+        if (ln >= 0) {
+            w.rng[k] = rs;
+            w.cnt[k] = cn | (ln << 16);
+            w.np[k] = (unsigned long long)(cn - 1) | ((unsigned long long)(cn * ln) << 32);
+            nbounce += (unsigned long long)(cn + ln);
+            k = -1;
+        }
     }
-    uint32_t rs = first ? (uint32_t)((int)i + 1) : w.rng[k];  // ResetRandom(i + 1), Renderer.cpp:42
-    if (first) { w.acc[3 * k] = 0.0f; w.acc[3 * k + 1] = 0.0f; w.acc[3 * k + 2] = 0.0f; }
-    // generate_paths (tpt_bdpt.h) with the vertices streamed into the records
-    const int cn = fill_path_rec<false>(s, w, k, 0, c0, c1, 1, rs, pk, stk);
-    // GenerateLightPath (BDPT.cpp:61-90) from m_emissionObjects[0]
-    const DObj lo = s.objs[s.emitters[0]];
-    V3 pc, pn;
-    int pp;
-    object_sample(s, lo, pc, pn, pp, rs);
-    BVert l0;
-    l0.x = pc; l0.N = pn; l0.type = T_LIGHT; l0.prim = pp; l0.mat = lo.mat;
-    l0.pdf = lo.pdf;
-    l0.alpha = divs(load_mat(s, lo.mat).em, l0.pdf);
-    l0.q1 = l0.q8 = 0.0f;
-    float pdf1;
-    V3 wi = cosine_sample(pn, pdf1, rs);
-    float ct = (float)dot3(l0.N, wi);
-    pdf1 = safe_div(pdf1, ct);
-    PTV it = scene_intersect(s, make_ray(l0.x, wi), TPT_CULL_BACK, stk);
-    BVert l1;
-    l1.x = it.x; l1.N = it.N; l1.type = it.type; l1.prim = it.prim;
-    l1.mat = it.prim >= 0 ? prim_mat(s, it.prim) : -1;
-    l1.pdf = srpdf_to_area(pdf1, T_LIGHT, l0.x, l0.N, it.type, it.x, it.N);
-    l1.alpha = v3s(0.0f);  // fresh InternalPathVertex (BDPT.hpp:19)
-    l1.q1 = l1.q8 = 0.0f;
-    if (pdf1 != 0.0f) l1.alpha = safe_div(l0.alpha, pdf1);
-    rec_store(w, kMaxLen, k, l0);
-    rec_store(w, kMaxLen + 1, k, l1);
-    const int ln = (pdf1 == 0.0f && it.type == T_BG) ? 2 : fill_path_rec<false>(s, w, k, kMaxLen, l0, l1, 1, rs, pk, stk);
-    w.rng[k] = rs;
-    w.cnt[k] = cn | (ln << 16);
-    w.np[k] = (unsigned long long)(cn - 1) | ((unsigned long long)(cn * ln) << 32);
-    atomicAdd(w.bounces, (unsigned long long)(cn + ln));
+    atomicAdd(w.bounces, nbounce);
 }
+
 
 // Canonical (t, s)-order range of pixel k's strategies and the starts of its two
 // task runs (s = 0 run in [0, n0_total), connecting run after it).
@@ -271,8 +309,9 @@ TPT_D StratRange strat_range(const WfState& w, int64_t k) {
     return r;
 }
 
-__global__ __launch_bounds__(kBlock) void tpt_bdpt_scatter_kernel(WfState w) {
+__global__ __launch_bounds__(kBlock) void tpt_bdpt_scatter_kernel(WfState w, unsigned* __restrict__ queue) {
     const int64_t k = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (k < 8) queue[k * 16] = 0;  // gen of the next iteration (same stream, after this kernel) starts its shards at 0
     if (k >= w.n) return;
     const StratRange r = strat_range(w, k);
     const int64_t n0_total = (int64_t)(w.incl[w.n - 1] & 0xffffffffull);
@@ -386,6 +425,8 @@ struct tpt_ctx {
     float* rows = nullptr;
     int64_t rows_cap = 0;
     unsigned long long* counters = nullptr;
+    unsigned* queue = nullptr;  // persistent gen: 8 shard counters, 64 B apart
+    int num_cu = 0;
     int pt_lanes = 8;  // Q: lanes per pixel of the PT kernel (1, 2, 4, 8, 16)
     // wavefront BDPT state (sized for wf_cap pixels)
     void* wf_mem = nullptr;
@@ -512,6 +553,15 @@ int launch(tpt_ctx* c, int mode, int spp, int64_t begin, int64_t stride, int64_t
         HIP_TRY(c, hipStreamWaitEvent(c->stream2, c->ev_fold[0], 0));  // stream2 starts after ev0
         const unsigned pblocks = (unsigned)((count + kBlock - 1) / kBlock);
         const unsigned cblocks = (unsigned)std::min<int64_t>(8192, (count * 24 + kBlock - 1) / kBlock + 1);
+        // persistent gen grid: as many workgroups as are resident at once, a multiple of
+        // the 8 queue shards, and no more than the pixels need
+        int per_cu = 0;
+        HIP_TRY(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                       &per_cu, lds ? (const void*)tpt_bdpt_gen_kernel<true> : (const void*)tpt_bdpt_gen_kernel<false>,
+                       kBlock, shmem));
+        int64_t gb = (int64_t)std::max(per_cu, 1) * std::max(c->num_cu, 1);
+        gb = std::min<int64_t>(gb, ((int64_t)pblocks + 7) / 8 * 8);
+        const unsigned gblocks = (unsigned)std::max<int64_t>(8, gb / 8 * 8);
         // connect walks the 4-wide shadow tree with a per-lane stack (shadow_q)
         DScene dsc = c->ds;
         dsc.max_stack = std::max(dsc.max_stack, dsc.q_stack);
@@ -526,15 +576,18 @@ int launch(tpt_ctx* c, int mode, int spp, int64_t begin, int64_t stride, int64_t
             w.n = count;
             w.bounces = c->counters;
             if (it >= 2) HIP_TRY(c, hipStreamWaitEvent(c->stream, c->ev_fold[b], 0));
+            if (it == 0) HIP_TRY(c, hipMemsetAsync(c->queue, 0, 8 * 64, c->stream));  // later: reset by scatter
             if (lds)
-                hipLaunchKernelGGL(tpt_bdpt_gen_kernel<true>, dim3(pblocks), dim3(kBlock), shmem, c->stream, c->ds, w, it);
+                hipLaunchKernelGGL(tpt_bdpt_gen_kernel<true>, dim3(gblocks), dim3(kBlock), shmem, c->stream, c->ds, w, it,
+                                   c->queue);
             else
-                hipLaunchKernelGGL(tpt_bdpt_gen_kernel<false>, dim3(pblocks), dim3(kBlock), shmem, c->stream, c->ds, w, it);
+                hipLaunchKernelGGL(tpt_bdpt_gen_kernel<false>, dim3(gblocks), dim3(kBlock), shmem, c->stream, c->ds, w, it,
+                                   c->queue);
             size_t bytes = c->scan_bytes;
             HIP_TRY(c, rocprim::inclusive_scan(c->scan_tmp, bytes, w.np, w.incl, (size_t)count,
                                                rocprim::plus<unsigned long long>(),
                                                c->stream));
-            hipLaunchKernelGGL(tpt_bdpt_scatter_kernel, dim3(pblocks), dim3(kBlock), 0, c->stream, w);
+            hipLaunchKernelGGL(tpt_bdpt_scatter_kernel, dim3(pblocks), dim3(kBlock), 0, c->stream, w, c->queue);
             HIP_TRY(c, hipEventRecord(c->ev_gen[b], c->stream));
             HIP_TRY(c, hipStreamWaitEvent(c->stream2, c->ev_gen[b], 0));
             if (lds)
@@ -659,7 +712,9 @@ int tpt_create(int device, tpt_ctx** out) {
         hipEventCreateWithFlags(&c->ev_gen[1], hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_fold[0], hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_fold[1], hipEventDisableTiming) != hipSuccess ||
-        hipMalloc(&c->counters, sizeof(unsigned long long) * 32) != hipSuccess) {
+        hipMalloc(&c->counters, sizeof(unsigned long long) * 32) != hipSuccess ||
+        hipMalloc(&c->queue, 8 * 64) != hipSuccess ||
+        hipDeviceGetAttribute(&c->num_cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) {
         delete c;
         return TPT_E_DEVICE;
     }
@@ -680,6 +735,7 @@ void tpt_destroy(tpt_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (void* p : {(void*)c->blob, (void*)c->rgb, (void*)c->splat, (void*)c->list, (void*)c->rows, (void*)c->counters,
+                    (void*)c->queue,
                     c->wf_mem, c->scan_tmp})
         if (p) (void)hipFree(p);
     if (c->stream2) (void)hipStreamSynchronize(c->stream2);
