@@ -76,6 +76,20 @@ TPT_D V3 eval_bsdf_sa(const DScene& s, int type, int mat, V3 x, V3 N, V3 pre, V3
     if (type == T_LIGHT || type == T_CAM) return v3s(1.0f);
     return eval_bsdf(load_mat(s, mat), normalized(pre - x), dir, normal_of(type, N), false);
 }
+// eval_bsdf_sa and eval_pdf_sa of the same vertex and direction together (bsdf_pdf).
+TPT_D void eval_pair_sa(const DScene& s, int type, int mat, V3 x, V3 N, V3 pre, V3 dir, V3& f, float& sr) {
+    const V3 n = normal_of(type, N);
+    float c = (float)dabs_(dot3(dir, n));
+    if (type == T_LIGHT || type == T_CAM) {
+        f = v3s(1.0f);
+        sr = type == T_LIGHT ? safe_div(cosine_pdf(n, dir), c) : kCamRayPdf;
+        return;
+    }
+    const V3 wo = normalized(pre - x);
+    float pdf;
+    bsdf_pdf(load_mat(s, mat), wo, dir, n, f, pdf);
+    sr = c == 0.0f ? 0.0f : safe_div(pdf, c);
+}
 // Append's pdf for `v` appended after `last` (whose predecessor is at `pre`), before
 // the RR factor (BDPT.cpp:154-158).
 TPT_D float append_pdf(const DScene& s, int ltype, int lmat, V3 lx, V3 lN, V3 pre, int vtype, V3 vx, V3 vN) {
@@ -174,6 +188,7 @@ TPT_D V3 path_weight(const DScene& s, const P& paths, int sl, int tl, Packet pk,
     const V3 lpre = sl >= 2 ? paths.lit(sl - 2).x : ly.x;
     TPT_STAMP(st, 1);
     V3 cst;
+    float srA0 = 0.0f, srB0 = 0.0f;  // set when sl >= 1
     if (sl == 0) {
         V3 wi = normalized(cpre - cz.x);
         V3 em = v3s(0.0f);  // PathVertex::Emission (BDPT.hpp:119-128)
@@ -184,10 +199,21 @@ TPT_D V3 path_weight(const DScene& s, const P& paths, int sl, int tl, Packet pk,
         float d2;
         V3 dir = normalize_len2(cz.x - ly.x, &d2);
         const bool shadowed = shadow_v<kPacket>(s, cz, ly, pk, stk);
+        if (s.dbg & 64) {
+            const unsigned long long act = __ballot(1), sh = __ballot(shadowed);
+            if (lane_id() == __builtin_ctzll(act)) {
+                atomicAdd(s.dbgc + 4, (unsigned long long)__popcll(act));
+                atomicAdd(s.dbgc + 5, (unsigned long long)__popcll(sh));
+            }
+        }
         TPT_STAMP(st, 2);
         if (shadowed) return v3s(0.0f);
-        V3 fl = eval_bsdf_sa(s, ly.type, ly.mat, ly.x, ly.N, lpre, dir);
-        V3 fc = eval_bsdf_sa(s, cz.type, cz.mat, cz.x, cz.N, cpre, -dir);
+        // each vertex's BSDF toward the other and the solid-angle pdf that Append
+        // computes for the same pair in loops A/B at k = 0 (ly -> cz: dir; cz -> ly:
+        // normalize(ly - cz) == -dir bit for bit), evaluated together
+        V3 fl, fc;
+        eval_pair_sa(s, ly.type, ly.mat, ly.x, ly.N, lpre, dir, fl, srB0);
+        eval_pair_sa(s, cz.type, cz.mat, cz.x, cz.N, cpre, -dir, fc, srA0);
         cst = mul(fl * fc, (float)dabs_(dot3(normal_of(ly.type, ly.N), dir) * dot3(normal_of(cz.type, cz.N), -dir) / (double)d2));
     }
     TPT_STAMP(st, 3);
@@ -201,7 +227,7 @@ TPT_D V3 path_weight(const DScene& s, const P& paths, int sl, int tl, Packet pk,
         } else {
             const BVert v = k == 0 ? ly : paths.lit(j);
             float pdf;
-            if (k == 0) pdf = append_pdf(s, cz.type, cz.mat, cz.x, cz.N, cpre, v.type, v.x, v.N);
+            if (k == 0) pdf = srpdf_to_area(srA0, cz.type, cz.x, cz.N, v.type, v.x, v.N);  // append_pdf(cz -> ly)
             else pdf = append_pdf(s, ly.type, ly.mat, ly.x, ly.N, cz.x, v.type, v.x, v.N);
             pdf *= rr_of(tl + k);
             cur *= safe_div(pdf, v.pdf);
@@ -224,7 +250,7 @@ TPT_D V3 path_weight(const DScene& s, const P& paths, int sl, int tl, Packet pk,
                 pdf = prim_pdf(s, v.prim);  // Append(count==0): vertex.obj->pdf(), no RR factor
             } else {
                 if (k == 0) {
-                    pdf = append_pdf(s, ly.type, ly.mat, ly.x, ly.N, lpre, v.type, v.x, v.N);
+                    pdf = srpdf_to_area(srB0, ly.type, ly.x, ly.N, v.type, v.x, v.N);  // append_pdf(ly -> cz), sl >= 1
                 } else {
                     // last = C[tl-1] as appended (type Light when it opened the path, BDPT.cpp:240-242)
                     const int at = sl == 0 ? T_LIGHT : cz.type;

@@ -35,7 +35,7 @@ extern __shared__ __align__(16) unsigned char tpt_smem[];
     pk.node = pk_node[threadIdx.x / 64];                                  \
     pk.mask = pk_mask[threadIdx.x / 64];
 
-// Workgroup prologue: LDS = [traversal stack: max_stack x kBlock ints][nodes][tris][qnodes][mats].
+// Workgroup prologue: LDS = [traversal stack: max_stack x kBlock ints][tnodes][tris][qnodes][mats].
 // With kLds the scene's node and triangle arrays are copied into LDS (16 B per lane
 // per step) and the kernel's DScene is pointed at them, so every traversal fetch is
 // a ds_read instead of a dependent L1/L2 load.
@@ -46,7 +46,7 @@ TPT_D int* stage_scene(DScene& s) {
         unsigned char* base = tpt_smem + (size_t)s.max_stack * kBlock * sizeof(int);
         const int nb = s.nnodes * (int)sizeof(DNode), tb = s.ntri * (int)sizeof(DTri),
                   qb = s.nqnodes * (int)sizeof(DQNode), mb = s.nmats * (int)sizeof(DMat);
-        const uint4* gn = reinterpret_cast<const uint4*>(s.nodes);
+        const uint4* gn = reinterpret_cast<const uint4*>(s.tnodes);
         const uint4* gt = reinterpret_cast<const uint4*>(s.tris);
         const uint4* gq = reinterpret_cast<const uint4*>(s.qnodes);
         uint4* ln = reinterpret_cast<uint4*>(base);
@@ -59,7 +59,7 @@ TPT_D int* stage_scene(DScene& s) {
         uint4* lm = reinterpret_cast<uint4*>(base + nb + tb + qb);
         for (int i = threadIdx.x; i < (mb + 15) / 16; i += kBlock) lm[i] = gm[i];  // 72-B records: round up
         __syncthreads();
-        s.nodes = reinterpret_cast<const DNode*>(base);
+        s.tnodes = reinterpret_cast<const DNode*>(base);  // the binary `nodes` stay in L1/L2 (light sampling)
         s.tris = reinterpret_cast<const DTri*>(base + nb);
         s.qnodes = reinterpret_cast<const DQNode*>(base + nb + tb);
         s.mats = reinterpret_cast<const DMat*>(base + nb + tb + qb);
@@ -344,6 +344,16 @@ __global__ __launch_bounds__(kBlock, TPT_CONN_MINWAVES) void tpt_bdpt_conn_kerne
         P.rec = rec_at(w.rec, k, 0);
         const V3 v = vmax0(path_weight<GlobPaths, false>(s, P, sl, t, pk, stk TPT_STAMPS_PASS));
         TPT_STAMP(st, 6);
+        if (s.dbg & 64) {  // strategy census: all / s = 0 / zero result
+            const unsigned long long act = __ballot(1), z = __ballot(v.x == 0.0f && v.y == 0.0f && v.z == 0.0f),
+                                     e = __ballot(sl == 0);
+            if (lane_id() == __builtin_ctzll(act)) {
+                atomicAdd(s.dbgc + 0, (unsigned long long)__popcll(act));
+                atomicAdd(s.dbgc + 1, (unsigned long long)__popcll(e));
+                atomicAdd(s.dbgc + 2, (unsigned long long)__popcll(z));
+                atomicAdd(s.dbgc + 3, (unsigned long long)__popcll(z & ~e));
+            }
+        }
         if (t > 1) {
             const int64_t ri = w.tres[g];
             w.res[3 * ri] = v.x;
@@ -643,6 +653,14 @@ int launch(tpt_ctx* c, int mode, int spp, int64_t begin, int64_t stride, int64_t
         std::fprintf(stderr, "[tpt dbg] bdpt waves %llu cycles/wave %.4g: camera %.1f%% light %.1f%% rev %.1f%% connect %.1f%%\n",
                      d[0], tot / d[0], 100.0 * d[1] / tot, 100.0 * d[2] / tot, 100.0 * d[3] / tot, 100.0 * d[4] / tot);
     }
+    if (c->ds.dbg & 64) {
+        unsigned long long d[8];
+        HIP_TRY(c, hipMemcpy(d, c->counters + 8, sizeof(d), hipMemcpyDeviceToHost));
+        std::fprintf(stderr, "[tpt dbg] strategies %llu: s=0 %.1f%%, zero result %.1f%% (connecting and zero %.1f%%); "
+                     "shadow tests %.1f%% of strategies, %.1f%% of them shadowed\n",
+                     d[0], 100.0 * d[1] / d[0], 100.0 * d[2] / d[0], 100.0 * d[3] / d[0], 100.0 * d[4] / d[0],
+                     100.0 * d[5] / d[4]);
+    }
     if (c->ds.dbg & 16) {
         unsigned long long d[8];
         HIP_TRY(c, hipMemcpy(d, c->counters + 8, sizeof(d), hipMemcpyDeviceToHost));
@@ -764,7 +782,7 @@ int tpt_upload_scene(tpt_ctx* c, const tpt_scene_desc* d) {
     size_t o_nodes = push_array(blob, hs.nodes), o_area = push_array(blob, hs.node_area),
            o_tris = push_array(blob, hs.tris), o_trix = push_array(blob, hs.trix), o_sph = push_array(blob, hs.sph),
            o_mats = push_array(blob, hs.mats), o_objs = push_array(blob, hs.objs),
-           o_em = push_array(blob, hs.emitters), o_q = push_array(blob, hs.qnodes);
+           o_em = push_array(blob, hs.emitters), o_q = push_array(blob, hs.qnodes), o_t = push_array(blob, hs.tnodes);
     if (c->blob) { (void)hipFree(c->blob); c->blob = nullptr; }
     HIP_TRY(c, hipMalloc(&c->blob, blob.size()));
     HIP_TRY(c, hipMemcpy(c->blob, blob.data(), blob.size(), hipMemcpyHostToDevice));
@@ -780,6 +798,7 @@ int tpt_upload_scene(tpt_ctx* c, const tpt_scene_desc* d) {
     ds.objs = (const DObj*)(b + o_objs);
     ds.emitters = (const int32_t*)(b + o_em);
     ds.qnodes = (const DQNode*)(b + o_q);
+    ds.tnodes = (const DNode*)(b + o_t);
     ds.nqnodes = (int)hs.qnodes.size();
     ds.nmats = (int)hs.mats.size();
     ds.n_emitters = (int)hs.emitters.size();
@@ -794,8 +813,10 @@ int tpt_upload_scene(tpt_ctx* c, const tpt_scene_desc* d) {
     ds.height = hs.height;
     ds.scale = camera_scale(hs.fov);
     for (int k = 0; k < 3; ++k) { ds.eye[k] = hs.eye[k]; ds.bg[k] = hs.bg[k]; }
-    ds.max_stack = hs.max_stack;
-    ds.q_stack = hs.q_stack;
+    // Per-lane walks are stackless (threaded tree); only the per-lane 4-wide shadow
+    // walk (TPT_LANE_SHADOW == 1, A/B builds) keeps an LDS stack.
+    ds.max_stack = TPT_LANE_SHADOW == 1 ? hs.max_stack : 0;
+    ds.q_stack = TPT_LANE_SHADOW == 1 ? hs.q_stack : 0;
     // Stage nodes + triangles + 4-wide nodes in LDS when they fit in 64 KB (the
     // Cornell presets need ~6 KB).
     {

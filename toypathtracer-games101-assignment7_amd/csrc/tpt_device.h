@@ -168,35 +168,36 @@ TPT_D bool sphere_test(const DSphere& s, const Ray& r, int cull, double& dist) {
 // (tpt_scene.h).  Same pop order (right child first), strict `>` on the f64
 // distance, so ties resolve exactly as in the reference.
 template <bool kFin>
-TPT_D Hit traverse_t(const DScene& s, int root, const Ray& r, int cull, int* stk) {
+TPT_D Hit traverse_t(const DScene& s, int root, const Ray& r, int cull, int* /*stk*/) {
+    // stackless walk of the threaded tree (tpt_scene.h): one node fetch per step
     Hit best;
     best.prim = -1;
     best.dist = 0.0;
-    if (root < 0) return best;
-    int sp = 0;
-    stk[0] = root;
-    sp = 1;
-    while (sp > 0) {
-        --sp;
-        const int ni = stk[sp * kBlock];
-        const DNode n = s.nodes[ni];
-        if (!box_hit_t<kFin>(n, r)) continue;
-        if (n.a >= 0) {
-            stk[sp * kBlock] = n.a;
-            stk[(sp + 1) * kBlock] = n.b;
-            sp += 2;
-            continue;
+    int cur = root, cont = kWalkEnd;
+    while (cur >= 0) {
+        const DNode n = s.tnodes[cur];
+        int nxt = n.b;
+        if (box_hit_t<kFin>(n, r)) {
+            if (n.a >= 0) {
+                if (n.a & kSpliceBit) {  // entering a mesh: resume at n.b when it is done
+                    cont = n.b;
+                    nxt = n.a & ~kSpliceBit;
+                } else {
+                    nxt = n.a;
+                }
+            } else if (n.a != kEmptyLeaf) {
+                const int prim = -1 - n.a;
+                double dist;
+                bool h;
+                if (prim < s.ntri) h = tri_test(s.tris[prim], r, cull, dist);
+                else h = sphere_test(s.sph[prim - s.ntri], r, cull, dist);
+                if (h && (best.prim < 0 || best.dist > dist)) {
+                    best.dist = dist;
+                    best.prim = prim;
+                }
+            }
         }
-        if (n.a == kEmptyLeaf) continue;
-        const int prim = -1 - n.a;
-        double dist;
-        bool h;
-        if (prim < s.ntri) h = tri_test(s.tris[prim], r, cull, dist);
-        else h = sphere_test(s.sph[prim - s.ntri], r, cull, dist);
-        if (h && (best.prim < 0 || best.dist > dist)) {
-            best.dist = dist;
-            best.prim = prim;
-        }
+        cur = nxt == kMeshExit ? cont : nxt;
     }
     return best;
 }
@@ -264,29 +265,32 @@ TPT_D bool box_overlap_q(const DQNode& q, int j, V3 lo, V3 hi) {
              (q.bmin[2][j] > hi.z) | (q.bmax[2][j] < lo.z));
 }
 template <bool kFin>
-TPT_D bool shadow_pts_walk(const DScene& s, const Ray& r, V3 lc, double thr, V3 lo, V3 hi, int cull, int* stk) {
-    int sp = 1;
-    stk[0] = 0;
-    while (sp > 0) {
-        --sp;
-        const DNode n = s.nodes[stk[sp * kBlock]];
-        if (!(box_overlap(n, lo, hi) & box_hit_t<kFin>(n, r))) continue;
-        if (n.a >= 0) {
-            stk[sp * kBlock] = n.a;
-            stk[(sp + 1) * kBlock] = n.b;
-            sp += 2;
-            continue;
+TPT_D bool shadow_pts_walk(const DScene& s, const Ray& r, V3 lc, double thr, V3 lo, V3 hi, int cull, int* /*stk*/) {
+    int cur = 0, cont = kWalkEnd;
+    while (cur >= 0) {
+        const DNode n = s.tnodes[cur];
+        int nxt = n.b;
+        if (box_overlap(n, lo, hi) & box_hit_t<kFin>(n, r)) {
+            if (n.a >= 0) {
+                if (n.a & kSpliceBit) {
+                    cont = n.b;
+                    nxt = n.a & ~kSpliceBit;
+                } else {
+                    nxt = n.a;
+                }
+            } else if (n.a != kEmptyLeaf) {
+                const int prim = -1 - n.a;
+                double dist;
+                bool h;
+                if (prim < s.ntri) h = tri_test(s.tris[prim], r, cull, dist);
+                else h = sphere_test(s.sph[prim - s.ntri], r, cull, dist);
+                if (h) {
+                    const V3 hx = r.o + mul(r.d, (float)dist);
+                    if (dot3(hx - lc, hx - lc) < thr) return true;
+                }
+            }
         }
-        if (n.a == kEmptyLeaf) continue;
-        const int prim = -1 - n.a;
-        double dist;
-        bool h;
-        if (prim < s.ntri) h = tri_test(s.tris[prim], r, cull, dist);
-        else h = sphere_test(s.sph[prim - s.ntri], r, cull, dist);
-        if (h) {
-            const V3 hx = r.o + mul(r.d, (float)dist);
-            if (dot3(hx - lc, hx - lc) < thr) return true;
-        }
+        cur = nxt == kMeshExit ? cont : nxt;
     }
     return false;
 }
@@ -828,6 +832,70 @@ TPT_D float mat_pdf(const Mat& m, V3 wo, V3 n, V3 wi) {
     return 0.0f;
 }
 
+// eval_bsdf(m, wo, wi, N, false) and mat_pdf(m, wo, N, wi) of one direction pair,
+// computed together: both start from the same nl, nv, half vector, n.h (ggx_d is
+// even in its argument, so GGXTerm(|n.h|) == GGXTerm(n.h)), v.h and l.h; only the
+// Fresnel argument differs (evalGivenSample uses fresnel(wi, h), pdf uses
+// fresnel(wo, h): Material.cpp:24 vs :112).  Same float ops as the two functions.
+TPT_D void bsdf_pdf(const Mat& m, V3 wo, V3 wi, V3 N, V3& f_out, float& pdf_out) {
+    f_out = v3s(0.0f);
+    pdf_out = 0.0f;
+    float nl = (float)dot3(N, wi);
+    float nv = (float)dot3(N, wo);
+    if (nl == 0.0f || nv == 0.0f) return;
+    V3 h = half_dir(N, wi, wo, m.ior_d);
+    const double dnh = dot3(N, h);
+    float nh = (float)dnh;
+    float lh = (float)dot3(wi, h);
+    float vh = (float)dot3(wo, h);
+    float D = ggx_d(nh, m.rough);
+    // ---- Material::pdf (Material.cpp:105-147)
+    {
+        V3 fp = fresnel(m, wo, h);
+        const double d = dabs_(dnh);
+        float pdf_h = (float)((double)D * d);  // ggx_half_pdf
+        float avh = fabs_(vh);
+        float ior_i, ior_o;
+        inout_ior(N, wi, wo, m.ior_d, ior_i, ior_o);
+        if (nv * nl < 0.0f) {
+            float den = ior_i * lh + ior_o * vh;
+            float jac = safe_div(ior_o * ior_o * avh, den * den);
+            if (m.type == TPT_TRANSPARENT) pdf_out = pdf_h * (1.0f - fp.x) * jac;
+        } else if (nv * nl > 0.0f) {
+            float jac = safe_div(1.0f, 4.0f * avh);
+            float diff = cosine_pdf(N, wi);
+            if (m.type == TPT_METAL) pdf_out = pdf_h * jac;
+            else if (m.type == TPT_DIELETRIC) pdf_out = (diff + pdf_h * jac) * 0.5f;
+            else pdf_out = pdf_h * fp.x * jac;
+        }
+    }
+    // ---- Material::evalGivenSample, combineCosineTerm = false (Material.cpp:11-72)
+    float G = ggx_vis(nv, vh, m.rough) * ggx_vis(nl, lh, m.rough);
+    V3 f = fresnel(m, wi, h);
+    if (nl * nv > 0.0f) {
+        V3 spec = v3s(0.0f);
+        if (G != 0.0f) {
+            spec = divs(mul(mul(f, D), G), (float)(4.0 * (double)fabs_(nv)));
+            spec = divs(spec, fabs_(nl));
+        }
+        V3 diff = v3s(0.0f);
+        if (m.type == TPT_DIELETRIC) diff = divs(m.kd * (v3s(1.0f) - f), kPi);
+        f_out = diff + spec;
+        return;
+    }
+    if (m.type != TPT_TRANSPARENT) return;
+    float ior_i, ior_o;
+    if (nv < 0.0f) { ior_i = 1.0f; ior_o = m.ior_d; }
+    else { ior_i = m.ior_d; ior_o = 1.0f; }
+    float pa = fabs_(vh) * fabs_(lh) / (fabs_(nv));
+    pa /= fabs_(nl);
+    float pb = ior_o * ior_o * (1.0f - f.x) * G * D;
+    if (pa * pb == 0.0f) return;
+    float pc = ior_i * lh + ior_o * vh;
+    pc *= pc;
+    f_out = v3s(pa * pb / pc);
+}
+
 // Material::sample (Material.cpp:150-214)
 TPT_D V3 mat_sample(const Mat& m, V3 wo, V3 n, float* pdf, uint32_t& rs) {
     V3 H = ggx_sample_h(n, m.rough, rs);
@@ -922,26 +990,25 @@ struct Hit2 {
 // NoCull and CullBack closest hits of one ray against one emitter object, one
 // traversal (same node order, same strict `>` tie rule for each result).
 template <bool kFin>
-TPT_D void mesh_hit_nocull_back(const DScene& s, int root, const Ray& r, Hit& hn, Hit& hb, int* stk) {
-    int sp = 1;
-    stk[0] = root;
-    while (sp > 0) {
-        --sp;
-        const DNode n = s.nodes[stk[sp * kBlock]];
-        if (!box_hit_t<kFin>(n, r)) continue;
-        if (n.a >= 0) {
-            stk[sp * kBlock] = n.a;
-            stk[(sp + 1) * kBlock] = n.b;
-            sp += 2;
-            continue;
+TPT_D void mesh_hit_nocull_back(const DScene& s, int root, const Ray& r, Hit& hn, Hit& hb, int* /*stk*/) {
+    int cur = root;  // a mesh subtree ends in kMeshExit
+    while (cur >= 0) {
+        const DNode n = s.tnodes[cur];
+        int nxt = n.b;
+        if (box_hit_t<kFin>(n, r)) {
+            if (n.a >= 0) {
+                nxt = n.a;
+            } else if (n.a != kEmptyLeaf) {
+                const int prim = -1 - n.a;
+                const DTri t = s.tris[prim];
+                double d;
+                if (tri_test(t, r, TPT_NO_CULL, d)) {  // culling is the test's first step
+                    if (hn.prim < 0 || hn.dist > d) { hn.prim = prim; hn.dist = d; }
+                    if (!(dot3(r.d, tri_normal(t)) > 0) && (hb.prim < 0 || hb.dist > d)) { hb.prim = prim; hb.dist = d; }
+                }
+            }
         }
-        if (n.a == kEmptyLeaf) continue;
-        const int prim = -1 - n.a;
-        const DTri t = s.tris[prim];
-        double d;
-        if (!tri_test(t, r, TPT_NO_CULL, d)) continue;  // culling is the test's first step
-        if (hn.prim < 0 || hn.dist > d) { hn.prim = prim; hn.dist = d; }
-        if (!(dot3(r.d, tri_normal(t)) > 0) && (hb.prim < 0 || hb.dist > d)) { hb.prim = prim; hb.dist = d; }
+        cur = nxt;
     }
 }
 TPT_D void object_hit_nocull_back(const DScene& s, const DObj& o, const Ray& r, Hit& hn, Hit& hb, int* stk) {

@@ -27,6 +27,19 @@ struct DNode {
 };
 static const int32_t kEmptyLeaf = (int32_t)0x80000000;
 
+// Threaded copy of `nodes` (same boxes, same 32-B layout, DNode with a = first,
+// b = next) for stackless per-lane walks in the reference's visit order (BVH.cpp:
+// 121-137 pushes left then right, so the right child is visited first):
+//   a >= 0: interior, a = the right child (kSpliceBit set: the node is a scene leaf
+//           replaced by its mesh's root -- entering the mesh, remember b);
+//   a <  0: leaf (-1 - prim, or kEmptyLeaf);
+//   b     : the node visited after this subtree (or after a box miss); kWalkEnd
+//           ends the walk, kMeshExit leaves a mesh subtree for the remembered node.
+// A walk therefore fetches one node per step and keeps no stack.
+static const int32_t kSpliceBit = 0x40000000;
+static const int32_t kWalkEnd = -1;
+static const int32_t kMeshExit = -2;
+
 // 128 B: a 4-wide node for shadow (any-hit) queries, made by collapsing two levels
 // of the binary tree (tpt_scene_build.cpp: build_qnodes).  Child j's box is the
 // binary node's own box; child >= 0 is another DQNode, child < 0 a leaf as in
@@ -95,6 +108,7 @@ struct DScene {
     const DObj* objs;
     const int32_t* emitters;  // Scene::m_emissionObjects (object ids)
     const DQNode* qnodes;     // 4-wide shadow tree, root at 0
+    const DNode* tnodes;      // threaded binary tree (stackless walks), same indices as nodes
     int32_t n_emitters;
     int32_t light_draws;  // XorShift draws of one DirectLightSampler::sample pass over all emitters
     int32_t ntri;

@@ -169,6 +169,31 @@ static int build_qnodes(HostScene& hs) {
     return build_q(hs, 0) & 0xff;
 }
 
+// Threading (tpt_scene.h, tnodes): node n's miss link is the node the reference's
+// DFS pops after n's subtree.  Scene-level nodes [0, ntop) are threaded as one
+// tree whose spliced mesh leaves keep their next link and point into the mesh;
+// every mesh subtree is threaded on its own and ends in kMeshExit.
+static void thread_tree(HostScene& hs, int n, int after, int ntop, bool scene) {
+    const DNode& src = hs.nodes[n];
+    DNode& t = hs.tnodes[n];
+    t = src;
+    t.b = after;
+    if (src.a < 0) return;  // leaf: a keeps the leaf code
+    const bool spliced = scene && src.a >= ntop;  // a scene leaf replaced by its mesh root
+    t.a = spliced ? (src.b | kSpliceBit) : src.b;  // right child first (BVH.cpp:129-132)
+    if (spliced) return;                            // the mesh is threaded by itself
+    thread_tree(hs, src.b, src.a, ntop, scene);    // after the right subtree: the left child
+    thread_tree(hs, src.a, after, ntop, scene);
+}
+
+static void build_threads(HostScene& hs, int ntop, const std::vector<int>& mesh_root) {
+    hs.tnodes.assign(hs.nodes.size(), DNode{});
+    if (hs.nodes.empty()) return;
+    thread_tree(hs, 0, kWalkEnd, ntop, true);
+    for (int r : mesh_root)
+        if (r >= 0) thread_tree(hs, r, kMeshExit, ntop, false);
+}
+
 int build_host_scene(const tpt_scene_desc* d, HostScene& hs, std::string& err) {
     hs = HostScene();
     if (!d || d->width <= 0 || d->height <= 0 || d->num_materials < 0 || d->num_objects < 0) {
@@ -349,6 +374,7 @@ int build_host_scene(const tpt_scene_desc* d, HostScene& hs, std::string& err) {
     hs.max_stack = max_depth + 1;
     // The 4-wide shadow tree pushes at most 3 entries per level of ceil(depth/2) levels.
     hs.q_stack = 3 * build_qnodes(hs) + 1;
+    build_threads(hs, ntop, mesh_base);
 
     // ---- objects and emitters
     for (int o = 0; o < d->num_objects; ++o) {

@@ -11,6 +11,7 @@ namespace tpt {
 struct HostScene {
     std::vector<DNode> nodes;
     std::vector<DQNode> qnodes;
+    std::vector<DNode> tnodes;
     std::vector<float> node_area;
     std::vector<DTri> tris;
     std::vector<DTriX> trix;
