@@ -21,6 +21,14 @@ namespace tpt {
 #define TPT_D __device__ __forceinline__
 
 constexpr int kBlock = 256;     // threads per workgroup (4 waves)
+// Segment culling for shadow walks (skip nodes whose box misses the padded AABB of
+// the shadow segment) is OFF: it assumes a computed hit point stays within the pad
+// of its triangle's box, but Moller-Trumbore's f32 cross products can move t by
+// ~2^-23 |tvec||e1||e2| / |det| on grazing rays, which no fixed pad bounds.  It
+// bought ~1.4 %.  Kept for A/B builds only (-DTPT_SEGMENT_CULL=1).
+#ifndef TPT_SEGMENT_CULL
+#define TPT_SEGMENT_CULL 0
+#endif
 constexpr int kStackCap = 64;   // max LDS stack entries per lane / per wave packet (upload rejects deeper trees)
 
 // ------------------------------------------------------------------ rays --
@@ -251,10 +259,8 @@ TPT_D PTV scene_intersect(const DScene& s, const Ray& r, int cull, int* stk) {
 // The hit point is lc + float(t)*d rounded per component and its squared distance
 // is summed in double: every step is monotone, so d2(t) is non-decreasing in t and
 // "closest hit's d2 < thr"  <=>  "some reachable hit's d2 < thr".  Hence an any-hit
-// traversal with early exit is exact.  A qualifying hit lies on the segment
-// [0, T], T ~ sqrt(thr); nodes whose box misses that segment's (padded) AABB cannot
-// contain one and are skipped.  Box tests themselves are the reference's, so the
-// set of reachable primitives is unchanged.
+// traversal with early exit is exact.  Box tests are the reference's, so the set
+// of reachable primitives is unchanged (segment culling: see TPT_SEGMENT_CULL).
 TPT_D bool box_overlap(const DNode& n, V3 lo, V3 hi) {
     return !((n.bmin[0] > hi.x) | (n.bmax[0] < lo.x) | (n.bmin[1] > hi.y) | (n.bmax[1] < lo.y) | (n.bmin[2] > hi.z) |
              (n.bmax[2] < lo.z));
@@ -303,8 +309,12 @@ TPT_D bool shadow_pts(const DScene& s, V3 lc, V3 x, int cull, int* stk) {
     const float T = sqrt_f((float)thr) * 1.0002f + 0.02f;  // segment-culling bound only
     const V3 e = v3(r.o.x + T * r.d.x, r.o.y + T * r.d.y, r.o.z + T * r.d.z);
     const float pad = 0.01f + 1e-4f * T;
+#if TPT_SEGMENT_CULL
     const V3 lo = v3(fminf(r.o.x, e.x) - pad, fminf(r.o.y, e.y) - pad, fminf(r.o.z, e.z) - pad);
     const V3 hi = v3(fmaxf(r.o.x, e.x) + pad, fmaxf(r.o.y, e.y) + pad, fmaxf(r.o.z, e.z) + pad);
+#else
+    const V3 lo = v3s(-3.40282347e+38f), hi = v3s(3.40282347e+38f);
+#endif
     return wave_finite(r) ? shadow_pts_walk<true>(s, r, lc, thr, lo, hi, cull, stk)
                           : shadow_pts_walk<false>(s, r, lc, thr, lo, hi, cull, stk);
 }
@@ -321,8 +331,12 @@ TPT_D bool shadow_q(const DScene& s, V3 lc, V3 x, int cull, int* stk) {
     const float T = (float)(sqrt_d(thr) * 1.0001 + 0.01);
     const V3 e = v3(r.o.x + T * r.d.x, r.o.y + T * r.d.y, r.o.z + T * r.d.z);
     const float pad = 0.01f + 1e-4f * T;
+#if TPT_SEGMENT_CULL
     const V3 lo = v3(fminf(r.o.x, e.x) - pad, fminf(r.o.y, e.y) - pad, fminf(r.o.z, e.z) - pad);
     const V3 hi = v3(fmaxf(r.o.x, e.x) + pad, fmaxf(r.o.y, e.y) + pad, fmaxf(r.o.z, e.z) + pad);
+#else
+    const V3 lo = v3s(-3.40282347e+38f), hi = v3s(3.40282347e+38f);
+#endif
     int sp = 1;
     stk[0] = 0;
     while (sp > 0) {
@@ -330,7 +344,8 @@ TPT_D bool shadow_q(const DScene& s, V3 lc, V3 x, int cull, int* stk) {
         const DQNode q = s.qnodes[stk[sp * kBlock]];
         bool hit[4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) hit[j] = box_overlap_q(q, j, lo, hi) & box_hit_q_finite(q, j, r);  // empty slots never overlap
+        for (int j = 0; j < 4; ++j)
+            hit[j] = (q.child[j] != kEmptyLeaf) & box_overlap_q(q, j, lo, hi) & box_hit_q_finite(q, j, r);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const int c = q.child[j];
@@ -391,8 +406,12 @@ TPT_D bool shadow_pts_packet(const DScene& s, V3 lc, V3 x, int cull, Packet pk, 
     const float T = (float)(sqrt_d(thr > 0.0 ? thr : 0.0) * 1.0001 + 0.01);
     const V3 e = v3(r.o.x + T * r.d.x, r.o.y + T * r.d.y, r.o.z + T * r.d.z);
     const float pad = 0.01f + 1e-4f * T;
+#if TPT_SEGMENT_CULL
     const V3 lo = v3(fminf(r.o.x, e.x) - pad, fminf(r.o.y, e.y) - pad, fminf(r.o.z, e.z) - pad);
     const V3 hi = v3(fmaxf(r.o.x, e.x) + pad, fmaxf(r.o.y, e.y) + pad, fmaxf(r.o.z, e.z) + pad);
+#else
+    const V3 lo = v3s(-3.40282347e+38f), hi = v3s(3.40282347e+38f);
+#endif
     unsigned long long live = uni64(__ballot(!done));
     if (live == 0) return shadowed;
     unsigned long long it_all = 0, it_leaf = 0;
@@ -476,8 +495,12 @@ TPT_D bool shadow_q_packet(const DScene& s, V3 lc, V3 x, int cull, Packet pk) {
     const float T = sqrt_f((float)(thr > 0.0 ? thr : 0.0)) * 1.0002f + 0.02f;
     const V3 e = v3(r.o.x + T * r.d.x, r.o.y + T * r.d.y, r.o.z + T * r.d.z);
     const float pad = 0.01f + 1e-4f * T;
+#if TPT_SEGMENT_CULL
     const V3 lo = v3(fminf(r.o.x, e.x) - pad, fminf(r.o.y, e.y) - pad, fminf(r.o.z, e.z) - pad);
     const V3 hi = v3(fmaxf(r.o.x, e.x) + pad, fmaxf(r.o.y, e.y) + pad, fmaxf(r.o.z, e.z) + pad);
+#else
+    const V3 lo = v3s(-3.40282347e+38f), hi = v3s(3.40282347e+38f);
+#endif
     unsigned long long live = uni64(__ballot(!done));
     unsigned long long it_all = 0, it_leaf = 0;
     if (live != 0) {
@@ -494,7 +517,7 @@ TPT_D bool shadow_q_packet(const DScene& s, V3 lc, V3 x, int cull, Packet pk) {
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     ch[j] = uni(q.child[j]);
-                    const bool h = mine & box_overlap_q(q, j, lo, hi) & box_hit_q_finite(q, j, r);
+                    const bool h = mine & (ch[j] != kEmptyLeaf) & box_overlap_q(q, j, lo, hi) & box_hit_q_finite(q, j, r);
                     mk[j] = uni64(__ballot(h));
                 }
                 int next = 0;
