@@ -261,6 +261,21 @@ TPT_D PTV scene_intersect(const DScene& s, const Ray& r, int cull, int* stk) {
 // "closest hit's d2 < thr"  <=>  "some reachable hit's d2 < thr".  Hence an any-hit
 // traversal with early exit is exact.  Box tests are the reference's, so the set
 // of reachable primitives is unchanged (segment culling: see TPT_SEGMENT_CULL).
+// Culling box of a shadow segment (TPT_SEGMENT_CULL, A/B only): everything when off.
+TPT_D void segment_box(const Ray& r, double thr, V3& lo, V3& hi) {
+#if TPT_SEGMENT_CULL
+    const float T = sqrt_f((float)(thr > 0.0 ? thr : 0.0)) * 1.0002f + 0.02f;
+    const V3 e = v3(r.o.x + T * r.d.x, r.o.y + T * r.d.y, r.o.z + T * r.d.z);
+    const float pad = 0.01f + 1e-4f * T;
+    lo = v3(fminf(r.o.x, e.x) - pad, fminf(r.o.y, e.y) - pad, fminf(r.o.z, e.z) - pad);
+    hi = v3(fmaxf(r.o.x, e.x) + pad, fmaxf(r.o.y, e.y) + pad, fmaxf(r.o.z, e.z) + pad);
+#else
+    (void)r;
+    (void)thr;
+    lo = v3s(-3.40282347e+38f);
+    hi = v3s(3.40282347e+38f);
+#endif
+}
 TPT_D bool box_overlap(const DNode& n, V3 lo, V3 hi) {
     return !((n.bmin[0] > hi.x) | (n.bmax[0] < lo.x) | (n.bmin[1] > hi.y) | (n.bmax[1] < lo.y) | (n.bmin[2] > hi.z) |
              (n.bmax[2] < lo.z));
@@ -306,15 +321,8 @@ TPT_D bool shadow_pts(const DScene& s, V3 lc, V3 x, int cull, int* stk) {
     const double thr = ld2 - 1.0f;
     if (!(thr > 0.0)) return false;  // d2 >= 0 can never be < thr
     const Ray r = make_ray(lc, normalized(x - lc));
-    const float T = sqrt_f((float)thr) * 1.0002f + 0.02f;  // segment-culling bound only
-    const V3 e = v3(r.o.x + T * r.d.x, r.o.y + T * r.d.y, r.o.z + T * r.d.z);
-    const float pad = 0.01f + 1e-4f * T;
-#if TPT_SEGMENT_CULL
-    const V3 lo = v3(fminf(r.o.x, e.x) - pad, fminf(r.o.y, e.y) - pad, fminf(r.o.z, e.z) - pad);
-    const V3 hi = v3(fmaxf(r.o.x, e.x) + pad, fmaxf(r.o.y, e.y) + pad, fmaxf(r.o.z, e.z) + pad);
-#else
-    const V3 lo = v3s(-3.40282347e+38f), hi = v3s(3.40282347e+38f);
-#endif
+    V3 lo, hi;
+    segment_box(r, thr, lo, hi);
     return wave_finite(r) ? shadow_pts_walk<true>(s, r, lc, thr, lo, hi, cull, stk)
                           : shadow_pts_walk<false>(s, r, lc, thr, lo, hi, cull, stk);
 }
@@ -328,15 +336,8 @@ TPT_D bool shadow_q(const DScene& s, V3 lc, V3 x, int cull, int* stk) {
     if (!(thr > 0.0)) return false;  // d2 >= 0 can never be < thr
     const Ray r = make_ray(lc, normalized(x - lc));
     if (!ray_monotone(r)) return shadow_pts(s, lc, x, cull, stk);
-    const float T = (float)(sqrt_d(thr) * 1.0001 + 0.01);
-    const V3 e = v3(r.o.x + T * r.d.x, r.o.y + T * r.d.y, r.o.z + T * r.d.z);
-    const float pad = 0.01f + 1e-4f * T;
-#if TPT_SEGMENT_CULL
-    const V3 lo = v3(fminf(r.o.x, e.x) - pad, fminf(r.o.y, e.y) - pad, fminf(r.o.z, e.z) - pad);
-    const V3 hi = v3(fmaxf(r.o.x, e.x) + pad, fmaxf(r.o.y, e.y) + pad, fmaxf(r.o.z, e.z) + pad);
-#else
-    const V3 lo = v3s(-3.40282347e+38f), hi = v3s(3.40282347e+38f);
-#endif
+    V3 lo, hi;
+    segment_box(r, thr, lo, hi);
     int sp = 1;
     stk[0] = 0;
     while (sp > 0) {
@@ -403,15 +404,8 @@ TPT_D bool shadow_pts_packet(const DScene& s, V3 lc, V3 x, int cull, Packet pk, 
     bool shadowed = false;
     if (s.dbg & 1) done = true;  // profiling ablation only
     const Ray r = make_ray(lc, normalized(x - lc));
-    const float T = (float)(sqrt_d(thr > 0.0 ? thr : 0.0) * 1.0001 + 0.01);
-    const V3 e = v3(r.o.x + T * r.d.x, r.o.y + T * r.d.y, r.o.z + T * r.d.z);
-    const float pad = 0.01f + 1e-4f * T;
-#if TPT_SEGMENT_CULL
-    const V3 lo = v3(fminf(r.o.x, e.x) - pad, fminf(r.o.y, e.y) - pad, fminf(r.o.z, e.z) - pad);
-    const V3 hi = v3(fmaxf(r.o.x, e.x) + pad, fmaxf(r.o.y, e.y) + pad, fmaxf(r.o.z, e.z) + pad);
-#else
-    const V3 lo = v3s(-3.40282347e+38f), hi = v3s(3.40282347e+38f);
-#endif
+    V3 lo, hi;
+    segment_box(r, thr, lo, hi);
     unsigned long long live = uni64(__ballot(!done));
     if (live == 0) return shadowed;
     unsigned long long it_all = 0, it_leaf = 0;
@@ -491,16 +485,8 @@ TPT_D bool shadow_q_packet(const DScene& s, V3 lc, V3 x, int cull, Packet pk) {
     const Ray r = make_ray(lc, normalized(x - lc));
     const bool slow = !done && !ray_monotone(r);
     if (slow) done = true;
-    // segment-culling bound only (no exactness role): f32 sqrt with a margin
-    const float T = sqrt_f((float)(thr > 0.0 ? thr : 0.0)) * 1.0002f + 0.02f;
-    const V3 e = v3(r.o.x + T * r.d.x, r.o.y + T * r.d.y, r.o.z + T * r.d.z);
-    const float pad = 0.01f + 1e-4f * T;
-#if TPT_SEGMENT_CULL
-    const V3 lo = v3(fminf(r.o.x, e.x) - pad, fminf(r.o.y, e.y) - pad, fminf(r.o.z, e.z) - pad);
-    const V3 hi = v3(fmaxf(r.o.x, e.x) + pad, fmaxf(r.o.y, e.y) + pad, fmaxf(r.o.z, e.z) + pad);
-#else
-    const V3 lo = v3s(-3.40282347e+38f), hi = v3s(3.40282347e+38f);
-#endif
+    V3 lo, hi;
+    segment_box(r, thr, lo, hi);
     unsigned long long live = uni64(__ballot(!done));
     unsigned long long it_all = 0, it_leaf = 0;
     if (live != 0) {
