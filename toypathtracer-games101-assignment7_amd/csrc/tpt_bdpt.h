@@ -105,19 +105,24 @@ TPT_D float prim_pdf(const DScene& s, int prim) {
     return prim < s.ntri ? 1.0f / s.trix[prim].area : 1.0f / s.sph[prim - s.ntri].area;
 }
 
-// Scene::ShadowCheck(const PTVertex&, const PTVertex&) (Scene.cpp:50-83)
-template <bool kPacket>
-TPT_D bool shadow_v(const DScene& s, const BVert& v1, const BVert& v2, Packet pk, int* stk) {
+// Scene::ShadowCheck(const PTVertex&, const PTVertex&) (Scene.cpp:50-83), the part
+// before the ray query: false when the reference answers "not shadowed" without a
+// query (Scene.cpp:71-78), otherwise the culling mode of the query (Scene.cpp:58-68).
+TPT_D bool shadow_query(const DScene& s, const BVert& v1, const BVert& v2, int& cull) {
     V3 atob = v2.x - v1.x;
-    bool test = true;
-    int cull = TPT_CULL_BACK;
+    cull = TPT_CULL_BACK;
     if (v1.prim >= 0 && v2.prim != v1.prim && s.mats[v1.mat].type == TPT_TRANSPARENT) {
         if (dot3(atob, v1.N) < 0.0f) cull = TPT_CULL_FRONT;
-    } else if (v1.prim >= 0 && dot3(atob, v1.N) < 0.0f) {
-        test = false;  // fast path "not shadowed" (Scene.cpp:71-74)
-    } else if (v2.prim >= 0 && dot3(-atob, v2.N) < 0.0f) {
-        test = false;  // Scene.cpp:75-78
+        return true;
     }
+    if (v1.prim >= 0 && dot3(atob, v1.N) < 0.0f) return false;  // fast path "not shadowed" (Scene.cpp:71-74)
+    if (v2.prim >= 0 && dot3(-atob, v2.N) < 0.0f) return false;  // Scene.cpp:75-78
+    return true;
+}
+template <bool kPacket>
+TPT_D bool shadow_v(const DScene& s, const BVert& v1, const BVert& v2, Packet pk, int* stk) {
+    int cull;
+    const bool test = shadow_query(s, v1, v2, cull);
     bool sh = false;
 #ifndef TPT_LANE_SHADOW
 #define TPT_LANE_SHADOW 0  // per-lane shadow walk: 0 binary tree, 1 4-wide tree, 2 wave packet on the 4-wide tree
@@ -198,16 +203,9 @@ TPT_D V3 path_weight(const DScene& s, const P& paths, int sl, int tl, Packet pk,
     } else {
         float d2;
         V3 dir = normalize_len2(cz.x - ly.x, &d2);
-        const bool shadowed = shadow_v<kPacket>(s, cz, ly, pk, stk);
-        if (s.dbg & 64) {
-            const unsigned long long act = __ballot(1), sh = __ballot(shadowed);
-            if (lane_id() == __builtin_ctzll(act)) {
-                atomicAdd(s.dbgc + 4, (unsigned long long)__popcll(act));
-                atomicAdd(s.dbgc + 5, (unsigned long long)__popcll(sh));
-            }
-        }
-        TPT_STAMP(st, 2);
-        if (shadowed) return v3s(0.0f);
+        // Scene::ShadowCheck (BDPT.cpp:205) is deferred to the end: a shadowed
+        // strategy returns 0, so the test only matters when the unshadowed result is
+        // not 0 (about a quarter of the tested strategies are 0 anyway).
         // each vertex's BSDF toward the other and the solid-angle pdf that Append
         // computes for the same pair in loops A/B at k = 0 (ly -> cz: dir; cz -> ly:
         // normalize(ly - cz) == -dir bit for bit), evaluated together
@@ -266,7 +264,25 @@ TPT_D V3 path_weight(const DScene& s, const P& paths, int sl, int tl, Packet pk,
     TPT_STAMP(st, 5);
     V3 lt = sl == 0 ? v3s(1.0f) : ly.alpha;
     V3 uc = lt * cz.alpha * cst;
-    return divs(uc, wd);
+    const V3 res = divs(uc, wd);
+    if (sl != 0) {
+        // Zero after the clamp either way (NaN compares false and is tested): +0 and
+        // -0 sum identically into the pixel (its sum starts at +0) and t = 1 splats
+        // skip zeros, so returning +0 without the test is exact.
+        const V3 c = vmax0(res);
+        if (c.x == 0.0f && c.y == 0.0f && c.z == 0.0f) return v3s(0.0f);
+        const bool shadowed = shadow_v<kPacket>(s, cz, ly, pk, stk);
+        if (s.dbg & 64) {
+            const unsigned long long act = __ballot(1), sh = __ballot(shadowed);
+            if (lane_id() == __builtin_ctzll(act)) {
+                atomicAdd(s.dbgc + 4, (unsigned long long)__popcll(act));
+                atomicAdd(s.dbgc + 5, (unsigned long long)__popcll(sh));
+            }
+        }
+        TPT_STAMP(st, 2);
+        if (shadowed) return v3s(0.0f);
+    }
+    return res;
 }
 
 // DrawToImage (SceneRenderingHelper.cpp:24-55), BlendMode::Additive, fp32 atomics.
@@ -481,8 +497,9 @@ TPT_D bool extend_rec(const DScene& s, const WfState& w, int64_t k, int base, BV
 // GenerateLightPath's first two vertices (BDPT.cpp:61-90, m_emissionObjects[0]),
 // stored at slots kMaxLen, kMaxLen + 1.  Returns false when the path ends there
 // (pdf1 == 0 and the ray escaped: ln = 2).
+template <bool kPacket>
 TPT_D bool light_start_rec(const DScene& s, const WfState& w, int64_t k, BVert& l0, BVert& l1, uint32_t& rs,
-                           int* stk) {
+                           Packet pk, int* stk) {
     const DObj lo = s.objs[s.emitters[0]];
     V3 pc, pn;
     int pp;
@@ -495,7 +512,8 @@ TPT_D bool light_start_rec(const DScene& s, const WfState& w, int64_t k, BVert& 
     V3 wi = cosine_sample(pn, pdf1, rs);
     float ct = (float)dot3(l0.N, wi);
     pdf1 = safe_div(pdf1, ct);
-    PTV it = scene_intersect(s, make_ray(l0.x, wi), TPT_CULL_BACK, stk);
+    const Ray lr = make_ray(l0.x, wi);
+    PTV it = kPacket ? scene_intersect_packet(s, lr, TPT_CULL_BACK, pk) : scene_intersect(s, lr, TPT_CULL_BACK, stk);
     l1.x = it.x; l1.N = it.N; l1.type = it.type; l1.prim = it.prim;
     l1.mat = it.prim >= 0 ? prim_mat(s, it.prim) : -1;
     l1.pdf = srpdf_to_area(pdf1, T_LIGHT, l0.x, l0.N, it.type, it.x, it.N);

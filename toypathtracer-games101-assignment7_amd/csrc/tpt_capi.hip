@@ -189,6 +189,9 @@ __global__ __launch_bounds__(kBlock) void tpt_bdpt_kernel(DScene s, int spp, int
 }
 
 // ---- wavefront BDPT kernels (see tpt_bdpt.h, "wavefront") --------------------
+#ifndef TPT_GEN_PACKET
+#define TPT_GEN_PACKET false  // wave-packet closest hits in gen (A/B)
+#endif
 #ifndef TPT_GEN_MINWAVES
 #define TPT_GEN_MINWAVES 4  // waves per SIMD (measured: 4 beats 3 and 5)
 #endif
@@ -262,7 +265,7 @@ __global__ __launch_bounds__(kBlock, TPT_GEN_MINWAVES) void tpt_bdpt_gen_kernel(
         int ln = -1;  // >= 0: the pixel's sample is complete
         if (phase == 1) {
             BVert l0, l1;
-            if (light_start_rec(s, w, k, l0, l1, rs, stk)) {
+            if (light_start_rec<TPT_GEN_PACKET>(s, w, k, l0, l1, rs, pk, stk)) {
                 prev = l0;
                 cur = l1;
                 i = 1;
@@ -271,7 +274,7 @@ __global__ __launch_bounds__(kBlock, TPT_GEN_MINWAVES) void tpt_bdpt_gen_kernel(
                 ln = 2;
             }
         }
-        if (ln < 0 && !extend_rec<false>(s, w, k, phase == 0 ? 0 : kMaxLen, prev, cur, i, rs, pk, stk)) {
+        if (ln < 0 && !extend_rec<TPT_GEN_PACKET>(s, w, k, phase == 0 ? 0 : kMaxLen, prev, cur, i, rs, pk, stk)) {
             if (phase == 0) {
                 cn = i + 1;
                 phase = 1;
@@ -447,6 +450,7 @@ struct tpt_ctx {
     void* scan_tmp = nullptr;
     size_t scan_bytes = 0;
     bool bdpt_mono = false;  // TPT_BDPT_KERNEL=mono: one lane per pixel stream (A/B only)
+    bool bdpt_serial = false;  // TPT_BDPT_SERIAL=1: connect/fold on the gen stream (per-kernel timing only)
 };
 
 namespace {
@@ -559,8 +563,9 @@ int launch(tpt_ctx* c, int mode, int spp, int64_t begin, int64_t stride, int64_t
         // beside connect(it) and fills the tail of each.  Ordering per pixel is kept:
         // gen is sequential on one stream (RNG state), fold is sequential on the other
         // (acc, splat), and buffer b is rewritten by gen(it+2) only after fold(it).
+        hipStream_t s2 = c->bdpt_serial ? c->stream : c->stream2;
         HIP_TRY(c, hipEventRecord(c->ev_fold[0], c->stream));
-        HIP_TRY(c, hipStreamWaitEvent(c->stream2, c->ev_fold[0], 0));  // stream2 starts after ev0
+        HIP_TRY(c, hipStreamWaitEvent(s2, c->ev_fold[0], 0));  // stream2 starts after ev0
         const unsigned pblocks = (unsigned)((count + kBlock - 1) / kBlock);
         const unsigned cblocks = (unsigned)std::min<int64_t>(8192, (count * 24 + kBlock - 1) / kBlock + 1);
         // persistent gen grid: as many workgroups as are resident at once, a multiple of
@@ -599,15 +604,15 @@ int launch(tpt_ctx* c, int mode, int spp, int64_t begin, int64_t stride, int64_t
                                                c->stream));
             hipLaunchKernelGGL(tpt_bdpt_scatter_kernel, dim3(pblocks), dim3(kBlock), 0, c->stream, w, c->queue);
             HIP_TRY(c, hipEventRecord(c->ev_gen[b], c->stream));
-            HIP_TRY(c, hipStreamWaitEvent(c->stream2, c->ev_gen[b], 0));
+            HIP_TRY(c, hipStreamWaitEvent(s2, c->ev_gen[b], 0));
             if (lds)
-                hipLaunchKernelGGL(tpt_bdpt_conn_kernel<true>, dim3(cblocks), dim3(kBlock), cshmem, c->stream2, dsc, w,
+                hipLaunchKernelGGL(tpt_bdpt_conn_kernel<true>, dim3(cblocks), dim3(kBlock), cshmem, s2, dsc, w,
                                    dsplat);
             else
-                hipLaunchKernelGGL(tpt_bdpt_conn_kernel<false>, dim3(cblocks), dim3(kBlock), cshmem, c->stream2, dsc,
+                hipLaunchKernelGGL(tpt_bdpt_conn_kernel<false>, dim3(cblocks), dim3(kBlock), cshmem, s2, dsc,
                                    w, dsplat);
-            hipLaunchKernelGGL(tpt_bdpt_fold_kernel, dim3(pblocks), dim3(kBlock), 0, c->stream2, w, inv);
-            HIP_TRY(c, hipEventRecord(c->ev_fold[b], c->stream2));
+            hipLaunchKernelGGL(tpt_bdpt_fold_kernel, dim3(pblocks), dim3(kBlock), 0, s2, w, inv);
+            HIP_TRY(c, hipEventRecord(c->ev_fold[b], s2));
         }
         HIP_TRY(c, hipStreamWaitEvent(c->stream, c->ev_fold[(spp - 1) & 1], 0));
         WfState w = c->wf[0];
@@ -829,6 +834,8 @@ int tpt_upload_scene(tpt_ctx* c, const tpt_scene_desc* d) {
         ds.dbgc = c->counters + 8;
         const char* bk = std::getenv("TPT_BDPT_KERNEL");
         c->bdpt_mono = bk && bk[0] == 'm';
+        const char* ser = std::getenv("TPT_BDPT_SERIAL");
+        c->bdpt_serial = ser && ser[0] == '1';
         const char* q = std::getenv("TPT_PT_LANES");
         c->pt_lanes = q ? std::atoi(q) : 8;  // Q = 8 measured best on one MI355X (Standard, 1024 spp)
         if (c->pt_lanes != 1 && c->pt_lanes != 2 && c->pt_lanes != 4 && c->pt_lanes != 8 && c->pt_lanes != 16) c->pt_lanes = 1;
