@@ -302,10 +302,64 @@ TPT_D void splat_add(const DScene& s, V3 light, V3 cam, V3 value, float* splat) 
             float w = smax(0.0f, 1.0f - dx) * smax(0.0f, 1.0f - dy);
             V3 c = mul(value, w);
             float* b = splat + 3 * ((int64_t)ix + (int64_t)s.height * iy);
+            if (s.dbg & (256 | 512)) {  // profiling: 256 skips the atomics, 512 counts them
+                if (s.dbg & 512) atomicAdd(s.dbgc + 6, (unsigned long long)((c.x != 0.0f) + (c.y != 0.0f) + (c.z != 0.0f)));
+                continue;
+            }
             if (c.x != 0.0f) atomicAdd(b + 0, c.x);
             if (c.y != 0.0f) atomicAdd(b + 1, c.y);
             if (c.z != 0.0f) atomicAdd(b + 2, c.z);
         }
+}
+
+// DrawToImage for the splats of a whole wave (call with every lane of the wave that
+// is still in the loop; `want` marks the lanes that have a splat).  Same float ops
+// per tap as splat_add, but the adds are regrouped: a splat touches a 3x3 block of
+// pixels = three row segments of 9 contiguous floats (rgb), so 27 lanes add one
+// splat with ONE atomic wave-instruction (two splats per instruction: lanes 0-26
+// and 32-58).  splat_add's per-lane form issues 64 adds to 64 scattered rows per
+// instruction, which the memory-side atomic unit serves ~17x slower per byte
+// (MI355X_MICROARCH.md, Global float atomics).  Only the summation order changes,
+// and fp32 atomics have no fixed order anyway.
+TPT_D void splat_wave(const DScene& s, bool want, V3 light, V3 cam, V3 value, float* splat) {
+    want = want && !(value.x == 0.0f && value.y == 0.0f && value.z == 0.0f);
+    float cx = 0.0f, cy = 0.0f;
+    if (want) {
+        V3 d = normalized(light - cam);
+        d = divs(d, d.z);
+        float aspect = (float)(s.width / s.height);
+        V3 t = v3(-d.x / s.scale / aspect, -d.y / s.scale, 0.0f);
+        V3 uv = mul(t + v3s(1.0f), 0.5f);
+        cx = uv.x * s.width;
+        cy = uv.y * s.height;
+    }
+    unsigned long long m = __ballot(want);
+    const int l = (int)__lane_id();
+    const int half = l >> 5, j = l & 31;
+    const int tap = j / 3, comp = j - 3 * tap;
+    const int ox = tap % 3 - 1, oy = tap / 3 - 1;
+    while (m != 0) {
+        const int a = __builtin_ctzll(m);
+        m &= m - 1;
+        const bool two = m != 0;  // a second splat for the upper half-wave
+        const int b = two ? __builtin_ctzll(m) : a;
+        if (two) m &= m - 1;
+        auto pick = [&](float v) {
+            const int va = __builtin_amdgcn_readlane(__float_as_int(v), a);
+            const int vb = __builtin_amdgcn_readlane(__float_as_int(v), b);
+            return __int_as_float(half ? vb : va);
+        };
+        const float px = pick(cx), py = pick(cy), vr = pick(value.x), vg = pick(value.y), vb = pick(value.z);
+        if (j < 27 && (!half || two)) {
+            const int ix = (int)px + ox, iy = (int)py + oy;
+            if (ix >= 0 && iy >= 0 && ix < s.width && iy < s.height) {
+                float dx = fabs_(px - (ix + 0.5f)), dy = fabs_(py - (iy + 0.5f));
+                float w = smax(0.0f, 1.0f - dx) * smax(0.0f, 1.0f - dy);
+                const float c = (comp == 0 ? vr : comp == 1 ? vg : vb) * w;
+                if (c != 0.0f) atomicAdd(splat + 3 * ((int64_t)ix + (int64_t)s.height * iy) + comp, c);
+            }
+        }
+    }
 }
 
 struct PrivPaths {  // paths held in the lane's private arrays

@@ -58,7 +58,12 @@ TPT_D int* stage_scene(DScene& s) {
         const uint4* gm = reinterpret_cast<const uint4*>(s.mats);
         uint4* lm = reinterpret_cast<uint4*>(base + nb + tb + qb);
         for (int i = threadIdx.x; i < (mb + 15) / 16; i += kBlock) lm[i] = gm[i];  // 72-B records: round up
+        const int lo = nb + tb + qb + ((mb + 15) & ~15), lb = s.nleaf * (int)sizeof(DNode);
+        const uint4* gl = reinterpret_cast<const uint4*>(s.leaves);
+        uint4* ll = reinterpret_cast<uint4*>(base + lo);
+        for (int i = threadIdx.x; i < lb / 16; i += kBlock) ll[i] = gl[i];
         __syncthreads();
+        s.leaves = reinterpret_cast<const DNode*>(base + lo);
         s.tnodes = reinterpret_cast<const DNode*>(base);  // the binary `nodes` stay in L1/L2 (light sampling)
         s.tris = reinterpret_cast<const DTri*>(base + nb);
         s.qnodes = reinterpret_cast<const DQNode*>(base + nb + tb);
@@ -327,6 +332,8 @@ __global__ __launch_bounds__(kBlock) void tpt_bdpt_scatter_kernel(WfState w, uns
     }
 }
 
+// One lane per strategy, grid-stride in wave-sized steps so that every lane of a
+// wave stays in the loop until the wave is done (splat_wave needs the whole wave).
 template <bool kLds>
 __global__ __launch_bounds__(kBlock, TPT_CONN_MINWAVES) void tpt_bdpt_conn_kernel(DScene s, WfState w, float* __restrict__ splat) {
     int* stk = stage_scene<kLds>(s);
@@ -338,33 +345,42 @@ __global__ __launch_bounds__(kBlock, TPT_CONN_MINWAVES) void tpt_bdpt_conn_kerne
     Stamps st{};
     st.last = stamp_now();
 #endif
-    for (int64_t g = (int64_t)blockIdx.x * kBlock + threadIdx.x; g < total; g += (int64_t)gridDim.x * kBlock) {
-        TPT_STAMP(st, 0);
-        const unsigned long long tk = w.task[g];
-        const int64_t k = (int64_t)(tk & 0xffffffffffull);
-        const int t = (int)((tk >> 40) & 0xff), sl = (int)(tk >> 48);
-        GlobPaths P;
-        P.rec = rec_at(w.rec, k, 0);
-        const V3 v = vmax0(path_weight<GlobPaths, false>(s, P, sl, t, pk, stk TPT_STAMPS_PASS));
-        TPT_STAMP(st, 6);
-        if (s.dbg & 64) {  // strategy census: all / s = 0 / zero result
-            const unsigned long long act = __ballot(1), z = __ballot(v.x == 0.0f && v.y == 0.0f && v.z == 0.0f),
-                                     e = __ballot(sl == 0);
-            if (lane_id() == __builtin_ctzll(act)) {
-                atomicAdd(s.dbgc + 0, (unsigned long long)__popcll(act));
-                atomicAdd(s.dbgc + 1, (unsigned long long)__popcll(e));
-                atomicAdd(s.dbgc + 2, (unsigned long long)__popcll(z));
-                atomicAdd(s.dbgc + 3, (unsigned long long)__popcll(z & ~e));
+    for (int64_t g0 = (int64_t)blockIdx.x * kBlock + (threadIdx.x & ~63); g0 < total;
+         g0 += (int64_t)gridDim.x * kBlock) {
+        const int64_t g = g0 + lane_id();
+        V3 v = v3s(0.0f), lx = eye;
+        bool sp = false;
+        if (g < total) {
+            TPT_STAMP(st, 0);
+            const unsigned long long tk = w.task[g];
+            const int64_t k = (int64_t)(tk & 0xffffffffffull);
+            const int t = (int)((tk >> 40) & 0xff), sl = (int)(tk >> 48);
+            GlobPaths P;
+            P.rec = rec_at(w.rec, k, 0);
+            v = vmax0(path_weight<GlobPaths, false>(s, P, sl, t, pk, stk TPT_STAMPS_PASS));
+            TPT_STAMP(st, 6);
+            if (s.dbg & 64) {  // strategy census: all / s = 0 / zero result
+                const unsigned long long act = __ballot(1), z = __ballot(v.x == 0.0f && v.y == 0.0f && v.z == 0.0f),
+                                         e = __ballot(sl == 0);
+                if (lane_id() == __builtin_ctzll(act)) {
+                    atomicAdd(s.dbgc + 0, (unsigned long long)__popcll(act));
+                    atomicAdd(s.dbgc + 1, (unsigned long long)__popcll(e));
+                    atomicAdd(s.dbgc + 2, (unsigned long long)__popcll(z));
+                    atomicAdd(s.dbgc + 3, (unsigned long long)__popcll(z & ~e));
+                }
+            }
+            if (t > 1) {
+                const int64_t ri = w.tres[g];
+                w.res[3 * ri] = v.x;
+                w.res[3 * ri + 1] = v.y;
+                w.res[3 * ri + 2] = v.z;
+            } else if (splat) {
+                sp = true;
+                lx = P.lit(sl - 1).x;
             }
         }
-        if (t > 1) {
-            const int64_t ri = w.tres[g];
-            w.res[3 * ri] = v.x;
-            w.res[3 * ri + 1] = v.y;
-            w.res[3 * ri + 2] = v.z;
-        } else if (splat) {
-            splat_add(s, P.lit(sl - 1).x, eye, v, splat);
-        }
+        // t = 1: DrawToImage of the light vertex (BDPT.cpp:303-305), whole wave
+        if (splat) splat_wave(s, sp, lx, eye, v, splat);
         TPT_STAMP(st, 7);
     }
 #ifdef TPT_STAMPS
@@ -374,6 +390,9 @@ __global__ __launch_bounds__(kBlock, TPT_CONN_MINWAVES) void tpt_bdpt_conn_kerne
 #endif
 }
 
+#ifndef TPT_FLAT_DEFAULT
+#define TPT_FLAT_DEFAULT 7  // measured: BDPT 882 -> 812 ms, PT 64.0 -> 61.3 ms
+#endif
 __global__ __launch_bounds__(kBlock) void tpt_bdpt_fold_kernel(WfState w, float inv) {
     const int64_t k = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (k >= w.n) return;
@@ -692,6 +711,17 @@ int launch(tpt_ctx* c, int mode, int spp, int64_t begin, int64_t stride, int64_t
         for (int x = 0; x < 12; ++x) std::fprintf(stderr, "[tpt stamps] %-16s %5.1f%%\n", nm[x], 100.0 * d[x] / tot);
     }
 #endif
+    if (c->ds.dbg & 512) {
+        unsigned long long d = 0;
+        HIP_TRY(c, hipMemcpy(&d, c->counters + 8 + 6, sizeof(d), hipMemcpyDeviceToHost));
+        std::fprintf(stderr, "[tpt dbg] splat atomics %llu (%.2f per sample)\n", d, (double)d / (double)(count * spp));
+    }
+    if (c->ds.dbg & 128) {  // per-lane shadow walk census (TPT_DEBUG_FLAGS & 128)
+        unsigned long long d[4];
+        HIP_TRY(c, hipMemcpy(d, c->counters + 8, sizeof(d), hipMemcpyDeviceToHost));
+        std::fprintf(stderr, "[tpt dbg] shadow walks: wave calls %llu, lanes/call %.1f, steps/lane %.2f, wave steps/call %.2f\n",
+                     d[0], (double)d[1] / d[0], (double)d[2] / d[1], (double)d[3] / d[0]);
+    }
     if (c->ds.dbg & 2) {  // profiling counters (TPT_DEBUG_FLAGS & 2)
         unsigned long long d[8];
         HIP_TRY(c, hipMemcpy(d, c->counters + 8, sizeof(d), hipMemcpyDeviceToHost));
@@ -787,7 +817,8 @@ int tpt_upload_scene(tpt_ctx* c, const tpt_scene_desc* d) {
     size_t o_nodes = push_array(blob, hs.nodes), o_area = push_array(blob, hs.node_area),
            o_tris = push_array(blob, hs.tris), o_trix = push_array(blob, hs.trix), o_sph = push_array(blob, hs.sph),
            o_mats = push_array(blob, hs.mats), o_objs = push_array(blob, hs.objs),
-           o_em = push_array(blob, hs.emitters), o_q = push_array(blob, hs.qnodes), o_t = push_array(blob, hs.tnodes);
+           o_em = push_array(blob, hs.emitters), o_q = push_array(blob, hs.qnodes), o_t = push_array(blob, hs.tnodes),
+           o_lf = push_array(blob, hs.leaves);
     if (c->blob) { (void)hipFree(c->blob); c->blob = nullptr; }
     HIP_TRY(c, hipMalloc(&c->blob, blob.size()));
     HIP_TRY(c, hipMemcpy(c->blob, blob.data(), blob.size(), hipMemcpyHostToDevice));
@@ -804,6 +835,8 @@ int tpt_upload_scene(tpt_ctx* c, const tpt_scene_desc* d) {
     ds.emitters = (const int32_t*)(b + o_em);
     ds.qnodes = (const DQNode*)(b + o_q);
     ds.tnodes = (const DNode*)(b + o_t);
+    ds.leaves = (const DNode*)(b + o_lf);
+    ds.nleaf = (int)hs.leaves.size();
     ds.nqnodes = (int)hs.qnodes.size();
     ds.nmats = (int)hs.mats.size();
     ds.n_emitters = (int)hs.emitters.size();
@@ -826,7 +859,8 @@ int tpt_upload_scene(tpt_ctx* c, const tpt_scene_desc* d) {
     // Cornell presets need ~6 KB).
     {
         const size_t sb = hs.nodes.size() * sizeof(DNode) + hs.tris.size() * sizeof(DTri) +
-                          ((hs.mats.size() * sizeof(DMat) + 15) & ~(size_t)15) + hs.qnodes.size() * sizeof(DQNode);
+                          ((hs.mats.size() * sizeof(DMat) + 15) & ~(size_t)15) + hs.qnodes.size() * sizeof(DQNode) +
+                          hs.leaves.size() * sizeof(DNode);
         const char* no = std::getenv("TPT_NO_LDS");
         ds.lds_bytes = (sb <= 64 * 1024 && !(no && no[0] == '1')) ? (int)sb : 0;
         const char* dbg = std::getenv("TPT_DEBUG_FLAGS");
@@ -836,6 +870,10 @@ int tpt_upload_scene(tpt_ctx* c, const tpt_scene_desc* d) {
         c->bdpt_mono = bk && bk[0] == 'm';
         const char* ser = std::getenv("TPT_BDPT_SERIAL");
         c->bdpt_serial = ser && ser[0] == '1';
+        // flat (all-leaves) queries for small scenes; TPT_FLAT overrides the bits (A/B)
+        const char* fl = std::getenv("TPT_FLAT");
+        ds.flat = fl ? std::atoi(fl) : TPT_FLAT_DEFAULT;
+        if (ds.nleaf > kFlatMaxLeaves || ds.lds_bytes == 0) ds.flat = 0;
         const char* q = std::getenv("TPT_PT_LANES");
         c->pt_lanes = q ? std::atoi(q) : 8;  // Q = 8 measured best on one MI355X (Standard, 1024 spp)
         if (c->pt_lanes != 1 && c->pt_lanes != 2 && c->pt_lanes != 4 && c->pt_lanes != 8 && c->pt_lanes != 16) c->pt_lanes = 1;

@@ -209,8 +209,63 @@ TPT_D Hit traverse_t(const DScene& s, int root, const Ray& r, int cull, int* /*s
     }
     return best;
 }
+// ---- flat queries: every primitive leaf box, no interior nodes ----------------
+// For a ray with finite inv the slab test is monotone in the box bounds (build_q in
+// tpt_scene_build.cpp) and every interior box is the union of its children's
+// (BVH.cpp:58-98), so a leaf's box passing implies every ancestor's box passes: the
+// primitives the reference tests are exactly those whose own leaf box passes.
+// Testing all leaf boxes in the reference's DFS leaf order (HostScene::leaves)
+// therefore visits the same primitives in the same relative order -- the same
+// closest hit, ties included (strict `>`), and the same any-hit answer.  The leaf
+// index is wave-uniform: no divergence in the loop, the primitive test runs only
+// when some lane's box passed.  For scenes with few leaves (the Cornell presets: 32
+// triangles) this beats a per-lane walk; rays with an infinite inv component keep
+// the walk.
+enum { kFlatShadow = 1, kFlatHit = 2, kFlatPkShadow = 4 };
+constexpr int kFlatMaxLeaves = 64;
+TPT_D Hit traverse_flat(const DScene& s, const Ray& r, int cull) {
+    Hit best;
+    best.prim = -1;
+    best.dist = 0.0;
+    for (int j = 0; j < s.nleaf; ++j) {
+        const DNode n = s.leaves[j];
+        if (slab_hit_finite(n.bmin[0], n.bmin[1], n.bmin[2], n.bmax[0], n.bmax[1], n.bmax[2], r)) {
+            const int prim = -1 - n.a;
+            double dist;
+            bool h;
+            if (prim < s.ntri) h = tri_test(s.tris[prim], r, cull, dist);
+            else h = sphere_test(s.sph[prim - s.ntri], r, cull, dist);
+            if (h && (best.prim < 0 || best.dist > dist)) {
+                best.dist = dist;
+                best.prim = prim;
+            }
+        }
+    }
+    return best;
+}
+// Any hit with |hit - lc|^2 < thr over all leaves (see shadow_pts for why any-hit is exact).
+TPT_D bool shadow_flat(const DScene& s, const Ray& r, V3 lc, double thr, int cull) {
+    for (int j = 0; j < s.nleaf; ++j) {
+        const DNode n = s.leaves[j];
+        if (slab_hit_finite(n.bmin[0], n.bmin[1], n.bmin[2], n.bmax[0], n.bmax[1], n.bmax[2], r)) {
+            const int prim = -1 - n.a;
+            double dist;
+            bool h;
+            if (prim < s.ntri) h = tri_test(s.tris[prim], r, cull, dist);
+            else h = sphere_test(s.sph[prim - s.ntri], r, cull, dist);
+            if (h) {
+                const V3 hx = r.o + mul(r.d, (float)dist);
+                if (dot3(hx - lc, hx - lc) < thr) return true;
+            }
+        }
+    }
+    return false;
+}
+
 TPT_D Hit traverse(const DScene& s, int root, const Ray& r, int cull, int* stk) {
-    return wave_finite(r) ? traverse_t<true>(s, root, r, cull, stk) : traverse_t<false>(s, root, r, cull, stk);
+    const bool fin = wave_finite(r);
+    if (fin && root == 0 && (s.flat & kFlatHit)) return traverse_flat(s, r, cull);
+    return fin ? traverse_t<true>(s, root, r, cull, stk) : traverse_t<false>(s, root, r, cull, stk);
 }
 
 // Intersection fields of a hit (Triangle.cpp:109-114, Sphere.cpp:30-36)
@@ -286,9 +341,11 @@ TPT_D bool box_overlap_q(const DQNode& q, int j, V3 lo, V3 hi) {
              (q.bmin[2][j] > hi.z) | (q.bmax[2][j] < lo.z));
 }
 template <bool kFin>
-TPT_D bool shadow_pts_walk(const DScene& s, const Ray& r, V3 lc, double thr, V3 lo, V3 hi, int cull, int* /*stk*/) {
+TPT_D bool shadow_pts_walk(const DScene& s, const Ray& r, V3 lc, double thr, V3 lo, V3 hi, int cull, int* /*stk*/,
+                           int& steps) {
     int cur = 0, cont = kWalkEnd;
     while (cur >= 0) {
+        ++steps;
         const DNode n = s.tnodes[cur];
         int nxt = n.b;
         if (box_overlap(n, lo, hi) & box_hit_t<kFin>(n, r)) {
@@ -323,8 +380,23 @@ TPT_D bool shadow_pts(const DScene& s, V3 lc, V3 x, int cull, int* stk) {
     const Ray r = make_ray(lc, normalized(x - lc));
     V3 lo, hi;
     segment_box(r, thr, lo, hi);
-    return wave_finite(r) ? shadow_pts_walk<true>(s, r, lc, thr, lo, hi, cull, stk)
-                          : shadow_pts_walk<false>(s, r, lc, thr, lo, hi, cull, stk);
+    int steps = 0;
+    const bool fin = wave_finite(r);
+    if (fin && (s.flat & kFlatShadow)) return shadow_flat(s, r, lc, thr, cull);
+    const bool sh = fin ? shadow_pts_walk<true>(s, r, lc, thr, lo, hi, cull, stk, steps)
+                        : shadow_pts_walk<false>(s, r, lc, thr, lo, hi, cull, stk, steps);
+    if (s.dbg & 128) {  // walk census: wave calls, active lanes, lane steps, wave steps (max over lanes)
+        int mx = steps;
+        for (int o = 32; o >= 1; o >>= 1) mx = max(mx, __shfl_xor(mx, o));
+        const unsigned long long act = __ballot(1);
+        atomicAdd(s.dbgc + 2, (unsigned long long)steps);
+        if ((int)__lane_id() == __builtin_ctzll(act)) {
+            atomicAdd(s.dbgc + 0, 1ull);
+            atomicAdd(s.dbgc + 1, (unsigned long long)__popcll(act));
+            atomicAdd(s.dbgc + 3, (unsigned long long)mx);
+        }
+    }
+    return sh;
 }
 
 // shadow_pts on the 4-wide tree (same answer, see build_q): one node fetch and four
@@ -483,6 +555,10 @@ TPT_D bool shadow_q_packet(const DScene& s, V3 lc, V3 x, int cull, Packet pk) {
     bool shadowed = false;
     if (s.dbg & 1) done = true;  // profiling ablation only
     const Ray r = make_ray(lc, normalized(x - lc));
+    if ((s.flat & kFlatPkShadow) && wave_finite(r)) {
+        if (!done) shadowed = shadow_flat(s, r, lc, thr, cull);
+        return shadowed;
+    }
     const bool slow = !done && !ray_monotone(r);
     if (slow) done = true;
     V3 lo, hi;

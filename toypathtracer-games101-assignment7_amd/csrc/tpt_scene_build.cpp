@@ -188,10 +188,32 @@ static void thread_tree(HostScene& hs, int n, int after, int ntop, bool scene) {
 
 static void build_threads(HostScene& hs, int ntop, const std::vector<int>& mesh_root) {
     hs.tnodes.assign(hs.nodes.size(), DNode{});
+    hs.leaves.clear();
     if (hs.nodes.empty()) return;
     thread_tree(hs, 0, kWalkEnd, ntop, true);
     for (int r : mesh_root)
         if (r >= 0) thread_tree(hs, r, kMeshExit, ntop, false);
+    // Leaves in the order a walk whose every box test passes visits them: the
+    // reference's DFS order (BVH.cpp:121-137) restricted to leaves.  Any subset of
+    // leaves a real ray reaches is visited in this relative order.
+    int cur = 0, cont = kWalkEnd;
+    while (cur >= 0) {
+        const DNode& n = hs.tnodes[cur];
+        int nxt = n.b;
+        if (n.a >= 0) {
+            if (n.a & kSpliceBit) {
+                cont = n.b;
+                nxt = n.a & ~kSpliceBit;
+            } else {
+                nxt = n.a;
+            }
+        } else if (n.a != kEmptyLeaf) {
+            DNode l = n;
+            l.b = 0;
+            hs.leaves.push_back(l);
+        }
+        cur = nxt == kMeshExit ? cont : nxt;
+    }
 }
 
 int build_host_scene(const tpt_scene_desc* d, HostScene& hs, std::string& err) {

@@ -12,6 +12,7 @@ struct HostScene {
     std::vector<DNode> nodes;
     std::vector<DQNode> qnodes;
     std::vector<DNode> tnodes;
+    std::vector<DNode> leaves;  // primitive leaves in the reference's visit order (flat queries)
     std::vector<float> node_area;
     std::vector<DTri> tris;
     std::vector<DTriX> trix;
