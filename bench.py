@@ -70,14 +70,23 @@ def cpu_baseline(mode, scene, threads):
     spp = 64 if mode == "pt" else 2
     m = 0 if mode == "pt" else 1
     if ref_available():
-        import contextlib
-        import io
-        R = Reference(scene)
-        buf = io.StringIO()
-        t0 = time.perf_counter()
-        with contextlib.redirect_stdout(buf):
+        # the reference prints its progress lines from C++ (fd 1): keep them off the
+        # bench's one-JSON-line stdout
+        sys.stdout.flush()
+        saved = os.dup(1)
+        devnull = os.open(os.devnull, os.O_WRONLY)
+        os.dup2(devnull, 1)
+        try:
+            R = Reference(scene)
+            t0 = time.perf_counter()
             R.render(m, spp, threads=threads)
-        dt = time.perf_counter() - t0
+            dt = time.perf_counter() - t0
+        finally:
+            import ctypes
+            ctypes.CDLL(None).fflush(None)  # C stdio buffers still hold reference output
+            os.dup2(saved, 1)
+            os.close(saved)
+            os.close(devnull)
         kind = "reference"
     else:
         o = Oracle(scene)
