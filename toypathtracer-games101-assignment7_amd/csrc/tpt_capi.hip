@@ -62,8 +62,13 @@ TPT_D int* stage_scene(DScene& s) {
         const uint4* gl = reinterpret_cast<const uint4*>(s.leaves);
         uint4* ll = reinterpret_cast<uint4*>(base + lo);
         for (int i = threadIdx.x; i < lb / 16; i += kBlock) ll[i] = gl[i];
+        const int go = lo + lb, gb = s.ngroup * (int)sizeof(DNode);
+        const uint4* gg = reinterpret_cast<const uint4*>(s.groups);
+        uint4* lg = reinterpret_cast<uint4*>(base + go);
+        for (int i = threadIdx.x; i < gb / 16; i += kBlock) lg[i] = gg[i];
         __syncthreads();
         s.leaves = reinterpret_cast<const DNode*>(base + lo);
+        s.groups = reinterpret_cast<const DNode*>(base + go);
         s.tnodes = reinterpret_cast<const DNode*>(base);  // the binary `nodes` stay in L1/L2 (light sampling)
         s.tris = reinterpret_cast<const DTri*>(base + nb);
         s.qnodes = reinterpret_cast<const DQNode*>(base + nb + tb);
@@ -818,7 +823,7 @@ int tpt_upload_scene(tpt_ctx* c, const tpt_scene_desc* d) {
            o_tris = push_array(blob, hs.tris), o_trix = push_array(blob, hs.trix), o_sph = push_array(blob, hs.sph),
            o_mats = push_array(blob, hs.mats), o_objs = push_array(blob, hs.objs),
            o_em = push_array(blob, hs.emitters), o_q = push_array(blob, hs.qnodes), o_t = push_array(blob, hs.tnodes),
-           o_lf = push_array(blob, hs.leaves);
+           o_lf = push_array(blob, hs.leaves), o_gr = push_array(blob, hs.groups);
     if (c->blob) { (void)hipFree(c->blob); c->blob = nullptr; }
     HIP_TRY(c, hipMalloc(&c->blob, blob.size()));
     HIP_TRY(c, hipMemcpy(c->blob, blob.data(), blob.size(), hipMemcpyHostToDevice));
@@ -837,6 +842,8 @@ int tpt_upload_scene(tpt_ctx* c, const tpt_scene_desc* d) {
     ds.tnodes = (const DNode*)(b + o_t);
     ds.leaves = (const DNode*)(b + o_lf);
     ds.nleaf = (int)hs.leaves.size();
+    ds.groups = (const DNode*)(b + o_gr);
+    ds.ngroup = (int)hs.groups.size();
     ds.nqnodes = (int)hs.qnodes.size();
     ds.nmats = (int)hs.mats.size();
     ds.n_emitters = (int)hs.emitters.size();
@@ -860,7 +867,7 @@ int tpt_upload_scene(tpt_ctx* c, const tpt_scene_desc* d) {
     {
         const size_t sb = hs.nodes.size() * sizeof(DNode) + hs.tris.size() * sizeof(DTri) +
                           ((hs.mats.size() * sizeof(DMat) + 15) & ~(size_t)15) + hs.qnodes.size() * sizeof(DQNode) +
-                          hs.leaves.size() * sizeof(DNode);
+                          (hs.leaves.size() + hs.groups.size()) * sizeof(DNode);
         const char* no = std::getenv("TPT_NO_LDS");
         ds.lds_bytes = (sb <= 64 * 1024 && !(no && no[0] == '1')) ? (int)sb : 0;
         const char* dbg = std::getenv("TPT_DEBUG_FLAGS");

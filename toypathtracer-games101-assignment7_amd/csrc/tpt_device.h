@@ -223,21 +223,30 @@ TPT_D Hit traverse_t(const DScene& s, int root, const Ray& r, int cull, int* /*s
 // the walk.
 enum { kFlatShadow = 1, kFlatHit = 2, kFlatPkShadow = 4 };
 constexpr int kFlatMaxLeaves = 64;
+// Objects are tested first (their box is the union of their leaves' boxes, so a
+// failed object box means every leaf box of it fails): a wave skips the leaves of an
+// object no lane's ray reaches.
 TPT_D Hit traverse_flat(const DScene& s, const Ray& r, int cull) {
     Hit best;
     best.prim = -1;
     best.dist = 0.0;
-    for (int j = 0; j < s.nleaf; ++j) {
-        const DNode n = s.leaves[j];
-        if (slab_hit_finite(n.bmin[0], n.bmin[1], n.bmin[2], n.bmax[0], n.bmax[1], n.bmax[2], r)) {
-            const int prim = -1 - n.a;
-            double dist;
-            bool h;
-            if (prim < s.ntri) h = tri_test(s.tris[prim], r, cull, dist);
-            else h = sphere_test(s.sph[prim - s.ntri], r, cull, dist);
-            if (h && (best.prim < 0 || best.dist > dist)) {
-                best.dist = dist;
-                best.prim = prim;
+    for (int gi = 0; gi < s.ngroup; ++gi) {
+        const DNode gn = s.groups[gi];
+        if (__ballot(slab_hit_finite(gn.bmin[0], gn.bmin[1], gn.bmin[2], gn.bmax[0], gn.bmax[1], gn.bmax[2], r)) == 0)
+            continue;
+        const int j1 = gn.a + gn.b;
+        for (int j = gn.a; j < j1; ++j) {
+            const DNode n = s.leaves[j];
+            if (slab_hit_finite(n.bmin[0], n.bmin[1], n.bmin[2], n.bmax[0], n.bmax[1], n.bmax[2], r)) {
+                const int prim = -1 - n.a;
+                double dist;
+                bool h;
+                if (prim < s.ntri) h = tri_test(s.tris[prim], r, cull, dist);
+                else h = sphere_test(s.sph[prim - s.ntri], r, cull, dist);
+                if (h && (best.prim < 0 || best.dist > dist)) {
+                    best.dist = dist;
+                    best.prim = prim;
+                }
             }
         }
     }
@@ -245,21 +254,29 @@ TPT_D Hit traverse_flat(const DScene& s, const Ray& r, int cull) {
 }
 // Any hit with |hit - lc|^2 < thr over all leaves (see shadow_pts for why any-hit is exact).
 TPT_D bool shadow_flat(const DScene& s, const Ray& r, V3 lc, double thr, int cull) {
-    for (int j = 0; j < s.nleaf; ++j) {
-        const DNode n = s.leaves[j];
-        if (slab_hit_finite(n.bmin[0], n.bmin[1], n.bmin[2], n.bmax[0], n.bmax[1], n.bmax[2], r)) {
-            const int prim = -1 - n.a;
-            double dist;
-            bool h;
-            if (prim < s.ntri) h = tri_test(s.tris[prim], r, cull, dist);
-            else h = sphere_test(s.sph[prim - s.ntri], r, cull, dist);
-            if (h) {
-                const V3 hx = r.o + mul(r.d, (float)dist);
-                if (dot3(hx - lc, hx - lc) < thr) return true;
+    bool sh = false;
+    for (int gi = 0; gi < s.ngroup; ++gi) {
+        const DNode gn = s.groups[gi];
+        if (__ballot(!sh && slab_hit_finite(gn.bmin[0], gn.bmin[1], gn.bmin[2], gn.bmax[0], gn.bmax[1], gn.bmax[2],
+                                            r)) == 0)
+            continue;
+        const int j1 = gn.a + gn.b;
+        for (int j = gn.a; j < j1; ++j) {
+            const DNode n = s.leaves[j];
+            if (!sh && slab_hit_finite(n.bmin[0], n.bmin[1], n.bmin[2], n.bmax[0], n.bmax[1], n.bmax[2], r)) {
+                const int prim = -1 - n.a;
+                double dist;
+                bool h;
+                if (prim < s.ntri) h = tri_test(s.tris[prim], r, cull, dist);
+                else h = sphere_test(s.sph[prim - s.ntri], r, cull, dist);
+                if (h) {
+                    const V3 hx = r.o + mul(r.d, (float)dist);
+                    if (dot3(hx - lc, hx - lc) < thr) sh = true;
+                }
             }
         }
     }
-    return false;
+    return sh;
 }
 
 TPT_D Hit traverse(const DScene& s, int root, const Ray& r, int cull, int* stk) {

@@ -110,7 +110,9 @@ struct DScene {
     const DQNode* qnodes;     // 4-wide shadow tree, root at 0
     const DNode* tnodes;      // threaded binary tree (stackless walks), same indices as nodes
     const DNode* leaves;      // primitive leaves in the reference's DFS order (flat queries)
+    const DNode* groups;      // leaves grouped per object: box, a = first leaf, b = count
     int32_t nleaf;
+    int32_t ngroup;
     int32_t flat;             // flat (all-leaves) queries: kFlatShadow | kFlatHit | kFlatPkShadow bits, 0 = tree walks
     int32_t n_emitters;
     int32_t light_draws;  // XorShift draws of one DirectLightSampler::sample pass over all emitters

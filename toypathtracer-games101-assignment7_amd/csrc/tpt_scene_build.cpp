@@ -196,6 +196,10 @@ static void build_threads(HostScene& hs, int ntop, const std::vector<int>& mesh_
     // Leaves in the order a walk whose every box test passes visits them: the
     // reference's DFS order (BVH.cpp:121-137) restricted to leaves.  Any subset of
     // leaves a real ray reaches is visited in this relative order.
+    // Leaves are grouped by object: a mesh's leaves are contiguous in that order and
+    // its group box is the scene-level leaf box (= the mesh root box); a sphere is a
+    // group of one.  groups[g] = {box, a = first leaf, b = leaf count}.
+    hs.groups.clear();
     int cur = 0, cont = kWalkEnd;
     while (cur >= 0) {
         const DNode& n = hs.tnodes[cur];
@@ -204,15 +208,31 @@ static void build_threads(HostScene& hs, int ntop, const std::vector<int>& mesh_
             if (n.a & kSpliceBit) {
                 cont = n.b;
                 nxt = n.a & ~kSpliceBit;
+                DNode g = n;
+                g.a = (int)hs.leaves.size();
+                g.b = 0;
+                hs.groups.push_back(g);
             } else {
                 nxt = n.a;
             }
         } else if (n.a != kEmptyLeaf) {
             DNode l = n;
             l.b = 0;
+            if (cur < ntop) {  // a leaf of the scene tree itself (sphere)
+                DNode g = n;
+                g.a = (int)hs.leaves.size();
+                g.b = 0;
+                hs.groups.push_back(g);
+            }
             hs.leaves.push_back(l);
+            hs.groups.back().b++;
         }
-        cur = nxt == kMeshExit ? cont : nxt;
+        if (nxt == kMeshExit) {
+            cur = cont;
+            cont = kWalkEnd;
+        } else {
+            cur = nxt;
+        }
     }
 }
 

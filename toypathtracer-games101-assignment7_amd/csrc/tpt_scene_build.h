@@ -13,6 +13,7 @@ struct HostScene {
     std::vector<DQNode> qnodes;
     std::vector<DNode> tnodes;
     std::vector<DNode> leaves;  // primitive leaves in the reference's visit order (flat queries)
+    std::vector<DNode> groups;  // per object: its box, first leaf (a) and leaf count (b)
     std::vector<float> node_area;
     std::vector<DTri> tris;
     std::vector<DTriX> trix;
