@@ -751,9 +751,26 @@ TPT_D V3 any_perp(V3 i) {
     }
     return normalized(v3(0.0f, 1.0f, -1.0f * i.y / i.z));
 }
+// Shading frame of a surface point seen from wo: the normal, the tangent frame
+// TransformVectorToWorld builds from it (SampleHelperFunctions.hpp:46-54:
+// t = AnyPerpendicular(n), b = n x t) and n.wo as the material code rounds it.  All
+// are functions of (n, wo) only, so a caller that shades the same point many times
+// (PT: every sample of a pixel) computes them once; the values are identical.
+struct Shade {
+    V3 n, t, b;
+    float nv;  // (float)DotProduct(n, wo)
+};
+TPT_D Shade make_shade(V3 n, V3 wo) {
+    Shade f;
+    f.n = n;
+    f.t = any_perp(n);
+    f.b = cross(n, f.t);
+    f.nv = (float)dot3(n, wo);
+    return f;
+}
 // TransformVectorToWorld (SampleHelperFunctions.hpp:46-54)
-TPT_D V3 to_world(V3 a, V3 n) {
-    V3 t = any_perp(n), b = cross(n, t);
+TPT_D V3 to_world(V3 a, const Shade& f) {
+    const V3 t = f.t, b = f.b, n = f.n;
     return v3(a.x * t.x + a.y * b.x + a.z * n.x, a.x * t.y + a.y * b.y + a.z * n.y,
               a.x * t.z + a.y * b.z + a.z * n.z);
 }
@@ -774,15 +791,18 @@ TPT_D V3 refract(V3 I, V3 N, float ior) {
     float k = 1 - eta * eta * (1 - cosi * cosi);
     return k < 0 ? v3s(0.0f) : normalized(mul(I, eta) + mul(n, eta * cosi - sqrt_f(k)));
 }
-// GetInsideOutsideIOR (SampleHelperFunctions.hpp:57-73)
-TPT_D void inout_ior(V3 N, V3 wi, V3 wo, float mior, float& ior_i, float& ior_o) {
-    float nl = (float)dot3(N, wi), nv = (float)dot3(N, wo);
+// GetInsideOutsideIOR (SampleHelperFunctions.hpp:57-73); nv = (float)DotProduct(N, wo)
+TPT_D void inout_ior(V3 N, V3 wi, float nv, float mior, float& ior_i, float& ior_o) {
+    float nl = (float)dot3(N, wi);
     ior_i = nl < 0.0f ? mior : 1.0f;
     ior_o = nv < 0.0f ? mior : 1.0f;
 }
-// GetHalfDir (SampleHelperFunctions.hpp:79-102)
-TPT_D V3 half_dir(V3 N, V3 wi, V3 wo, float mior) {
-    float nl = (float)dot3(N, wi), nv = (float)dot3(N, wo);
+TPT_D void inout_ior(V3 N, V3 wi, V3 wo, float mior, float& ior_i, float& ior_o) {
+    inout_ior(N, wi, (float)dot3(N, wo), mior, ior_i, ior_o);
+}
+// GetHalfDir (SampleHelperFunctions.hpp:79-102); nv = (float)DotProduct(N, wo)
+TPT_D V3 half_dir(V3 N, V3 wi, V3 wo, float nv, float mior) {
+    float nl = (float)dot3(N, wi);
     if (nl == 0.0f || nv == 0.0f) return v3s(0.0f);
     if (nl * nv > 0.0f) {
         V3 h = normalized(wi + wo);
@@ -791,18 +811,21 @@ TPT_D V3 half_dir(V3 N, V3 wi, V3 wo, float mior) {
     if (nv < 0.0f) return -normalized(mul(wo, mior) + wi);
     return -normalized(wo + mul(wi, mior));
 }
+TPT_D V3 half_dir(V3 N, V3 wi, V3 wo, float mior) { return half_dir(N, wi, wo, (float)dot3(N, wo), mior); }
 // GetCosineWeightedSample (SampleHelperFunctions.hpp:105-115); cos/sin in double
-TPT_D V3 cosine_sample(V3 N, float& pdf, uint32_t& rs) {
+TPT_D V3 cosine_sample(const Shade& f, float& pdf, uint32_t& rs) {
+    const V3 N = f.n;
     float u1 = rng_float(rs);
     float r = sqrt_f(u1);
     float theta = 2 * kPi * rng_float(rs);
     double sd, cd;
     tpt_sincos_d((double)theta, &sd, &cd);
     float x = (float)((double)r * cd), y = (float)((double)r * sd);
-    V3 wi = normalized(to_world(v3(x, y, sqrt_f(1.0f - u1)), N));
+    V3 wi = normalized(to_world(v3(x, y, sqrt_f(1.0f - u1)), f));
     pdf = (float)(dot3(wi, N) / (double)kPi);
     return wi;
 }
+TPT_D V3 cosine_sample(V3 N, float& pdf, uint32_t& rs) { return cosine_sample(make_shade(N, N), pdf, rs); }
 // GetCosineWeightedPdf (SampleHelperFunctions.hpp:118-120)
 TPT_D float cosine_pdf(V3 N, V3 wi) { return saturate((float)dot3(wi, N)) / kPi; }
 
@@ -829,7 +852,7 @@ TPT_D float ggx_half_pdf(V3 n, V3 h, float r) {
     return (float)((double)ggx_d((float)d, r) * d);
 }
 // GGX.hpp:46-59
-TPT_D V3 ggx_sample_h(V3 N, float r, uint32_t& rs) {
+TPT_D V3 ggx_sample_h(const Shade& f, float r, uint32_t& rs) {
     float d1 = rng_float(rs), d2 = rng_float(rs);
     float theta = tpt_atan2f(r * sqrt_f(d1), sqrt_f(1.0f - d1));
     float phi = 2.0f * kPi * d2;
@@ -837,7 +860,7 @@ TPT_D V3 ggx_sample_h(V3 N, float r, uint32_t& rs) {
     tpt_sincosf(theta, &st, &ct);
     tpt_sincosf(phi, &sp, &cp);
     V3 local = v3(st * cp, st * sp, ct);
-    return normalized(to_world(local, N));
+    return normalized(to_world(local, f));
 }
 
 // Material::fresnel (Material.cpp:221-252)
@@ -866,11 +889,12 @@ TPT_D V3 fresnel(const Mat& m, V3 I, V3 N) {
 }
 
 // Material::evalGivenSample (Material.cpp:11-72)
-TPT_D V3 eval_bsdf(const Mat& m, V3 wo, V3 wi, V3 N, bool cosine) {
+TPT_D V3 eval_bsdf(const Mat& m, V3 wo, V3 wi, const Shade& sh, bool cosine) {
+    const V3 N = sh.n;
     float nl = (float)dot3(N, wi);
-    float nv = (float)dot3(N, wo);
+    float nv = sh.nv;
     if (nl == 0.0f || nv == 0.0f) return v3s(0.0f);
-    V3 h = half_dir(N, wi, wo, m.ior_d);
+    V3 h = half_dir(N, wi, wo, nv, m.ior_d);
     float nh = (float)dot3(N, h);
     float lh = (float)dot3(wi, h);
     float vh = (float)dot3(wo, h);
@@ -902,22 +926,26 @@ TPT_D V3 eval_bsdf(const Mat& m, V3 wo, V3 wi, V3 N, bool cosine) {
     pc *= pc;
     return v3s(pa * pb / pc);
 }
+TPT_D V3 eval_bsdf(const Mat& m, V3 wo, V3 wi, V3 N, bool cosine) {
+    return eval_bsdf(m, wo, wi, make_shade(N, wo), cosine);
+}
 
 TPT_D float safe_div(float v, float p) { return p == 0.0f ? 0.0f : v / p; }  // SampleHelperFunctions.hpp:24-32
 TPT_D V3 safe_div(V3 v, float p) { return p == 0.0f ? v3s(0.0f) : divs(v, p); }
 
 // Material::pdf (Material.cpp:105-147)
-TPT_D float mat_pdf(const Mat& m, V3 wo, V3 n, V3 wi) {
-    float nv = (float)dot3(n, wo), nl = (float)dot3(n, wi);
+TPT_D float mat_pdf(const Mat& m, V3 wo, const Shade& sh, V3 wi) {
+    const V3 n = sh.n;
+    float nv = sh.nv, nl = (float)dot3(n, wi);
     if (nv == 0.0f || nl == 0.0f) return 0.0f;
-    V3 h = half_dir(n, wi, wo, m.ior_d);
+    V3 h = half_dir(n, wi, wo, nv, m.ior_d);
     V3 f = fresnel(m, wo, h);
     float pdf_h = ggx_half_pdf(n, h, m.rough);
     float vh = (float)dot3(wo, h);
     float avh = fabs_(vh);
     float lh = (float)dot3(wi, h);
     float ior_i, ior_o;
-    inout_ior(n, wi, wo, m.ior_d, ior_i, ior_o);
+    inout_ior(n, wi, nv, m.ior_d, ior_i, ior_o);
     if (nv * nl < 0.0f) {
         float den = ior_i * lh + ior_o * vh;
         float jac = safe_div(ior_o * ior_o * avh, den * den);
@@ -933,6 +961,7 @@ TPT_D float mat_pdf(const Mat& m, V3 wo, V3 n, V3 wi) {
     }
     return 0.0f;
 }
+TPT_D float mat_pdf(const Mat& m, V3 wo, V3 n, V3 wi) { return mat_pdf(m, wo, make_shade(n, wo), wi); }
 
 // eval_bsdf(m, wo, wi, N, false) and mat_pdf(m, wo, N, wi) of one direction pair,
 // computed together: both start from the same nl, nv, half vector, n.h (ggx_d is
@@ -999,11 +1028,12 @@ TPT_D void bsdf_pdf(const Mat& m, V3 wo, V3 wi, V3 N, V3& f_out, float& pdf_out)
 }
 
 // Material::sample (Material.cpp:150-214)
-TPT_D V3 mat_sample(const Mat& m, V3 wo, V3 n, float* pdf, uint32_t& rs) {
-    V3 H = ggx_sample_h(n, m.rough, rs);
+TPT_D V3 mat_sample(const Mat& m, V3 wo, const Shade& sh, float* pdf, uint32_t& rs) {
+    const V3 n = sh.n;
+    V3 H = ggx_sample_h(sh, m.rough, rs);
     V3 wis = reflect(wo, H);
     float pdf_h = ggx_half_pdf(n, H, m.rough);
-    float vn = (float)dot3(wo, n);
+    float vn = sh.nv;  // (float)DotProduct(wo, n)
     float vh = (float)dot3(wo, H);
     float avh = fabs_(vh);
     float jr = safe_div(1.0f, 4.0f * avh);
@@ -1020,7 +1050,7 @@ TPT_D V3 mat_sample(const Mat& m, V3 wo, V3 n, float* pdf, uint32_t& rs) {
             return wis;
         }
         float pd;
-        V3 wid = cosine_sample(n, pd, rs);
+        V3 wid = cosine_sample(sh, pd, rs);
         H = normalized(wid + wo);
         vh = (float)dot3(wo, H);
         avh = fabs_(vh);
@@ -1038,13 +1068,16 @@ TPT_D V3 mat_sample(const Mat& m, V3 wo, V3 n, float* pdf, uint32_t& rs) {
     }
     V3 wr = refract(wo, H, m.ior_d);
     float ior_i, ior_o;
-    inout_ior(n, wr, wo, m.ior_d, ior_i, ior_o);
+    inout_ior(n, wr, vn, m.ior_d, ior_i, ior_o);
     float lh = (float)dot3(wr, H);
     float den = ior_i * lh + ior_o * vh;
     float jt = safe_div(ior_o * ior_o * avh, den * den);
     *pdf = pdf_h * (1.0f - f.x) * jt;
     if ((double)vn * dot3(wr, n) > 0.0f) *pdf = 0.0f;
     return wr;
+}
+TPT_D V3 mat_sample(const Mat& m, V3 wo, V3 n, float* pdf, uint32_t& rs) {
+    return mat_sample(m, wo, make_shade(n, wo), pdf, rs);
 }
 
 // ---------------------------------------------------------- light objects --
@@ -1184,7 +1217,10 @@ enum PixSlot {
     kPxWo = kPxN + 3,
     kPxKdM = kPxWo + 3,   // Dieletric: Kd; Metal: ior_m (each type reads only its own)
     kPxIorMK = kPxKdM + 3,
-    kPixSlots = kPxIorMK + 3
+    kPxT = kPxIorMK + 3,  // Shade of the camera hit: tangent, bitangent, n.wo
+    kPxB = kPxT + 3,
+    kPxNv = kPxB + 3,
+    kPixSlots = kPxNv + 1
 };
 struct PixPark {
     float* base;  // kPixSlots x kBlock floats of LDS
@@ -1198,6 +1234,14 @@ struct PixPark {
         return v3(p[k * kBlock], p[(k + 1) * kBlock], p[(k + 2) * kBlock]);
     }
     TPT_D int mat_index() const { return __float_as_int(lane()[kPxMat * kBlock]); }
+    TPT_D Shade shade() const {
+        Shade f;
+        f.n = v(kPxN);
+        f.t = v(kPxT);
+        f.b = v(kPxB);
+        f.nv = lane()[kPxNv * kBlock];
+        return f;
+    }
     TPT_D Mat mat() const {
         const float* p = lane();
         Mat m;
@@ -1226,6 +1270,10 @@ struct PixPark {
         put3(kPxWo, wo);
         put3(kPxKdM, m.type == TPT_METAL ? m.ior_m : m.kd);
         put3(kPxIorMK, m.ior_m_k);
+        const Shade f = make_shade(n, wo);
+        put3(kPxT, f.t);
+        put3(kPxB, f.b);
+        put(kPxNv, f.nv);
     }
 };
 
@@ -1240,7 +1288,7 @@ TPT_D V3 pt_sample(const DScene& s, PixPark px, uint32_t& rs, int* stk, Packet p
         if (dm.has_em) result = result + v3(dm.em[0], dm.em[1], dm.em[2]);
     }
     float pdf_b;
-    V3 wib = mat_sample(px.mat(), px.v(kPxWo), px.v(kPxN), &pdf_b, rs);
+    V3 wib = mat_sample(px.mat(), px.v(kPxWo), px.shade(), &pdf_b, rs);
     TPT_STAMP(st, 1);
     for (int li = 0; li < s.n_emitters; ++li) {
         const DObj o = s.objs[s.emitters[li]];
@@ -1278,13 +1326,13 @@ TPT_D V3 pt_sample(const DScene& s, PixPark px, uint32_t& rs, int* stk, Packet p
                     const bool sh = shadow_q_packet(s, hx, px.v(kPxX), TPT_CULL_BACK, pk);
                     TPT_STAMP(st, 5);
                     if (!sh)
-                        ev = ev + divs(eval_bsdf(px.mat(), px.v(kPxWo), wib, px.v(kPxN), true), 1e-4f + pdf_b + pbl);
+                        ev = ev + divs(eval_bsdf(px.mat(), px.v(kPxWo), wib, px.shade(), true), 1e-4f + pdf_b + pbl);
                     TPT_STAMP(st, 6);
                 }
             }
         }
         // the light branch (PathTracer.cpp:95-106); plb is pure, so it is computed here
-        float plb = mat_pdf(px.mat(), px.v(kPxWo), px.v(kPxN), wil);
+        float plb = mat_pdf(px.mat(), px.v(kPxWo), px.shade(), wil);
         TPT_STAMP(st, 7);
         if (pll + plb > 0.0f) {
             Ray rl = make_ray(px.v(kPxX), wil);
@@ -1295,7 +1343,7 @@ TPT_D V3 pt_sample(const DScene& s, PixPark px, uint32_t& rs, int* stk, Packet p
             const bool sh = shadow_q_packet(s, hx, px.v(kPxX), TPT_CULL_BACK, pk);
             TPT_STAMP(st, 9);
             if (!sh)
-                ev = ev + divs(eval_bsdf(px.mat(), px.v(kPxWo), wil, px.v(kPxN), true), 1e-4f + pll + plb);
+                ev = ev + divs(eval_bsdf(px.mat(), px.v(kPxWo), wil, px.shade(), true), 1e-4f + pll + plb);
             TPT_STAMP(st, 10);
         }
         result = result + ev * load_mat(s, o.mat).em;
