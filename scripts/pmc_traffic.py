@@ -22,7 +22,7 @@ import os
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def per_launch(path, kernel, counter):
+def per_launch(path, kernel, counter, frames=None):
     tot, disp = 0.0, set()
     for r in csv.DictReader(open(path)):
         if kernel in r["Kernel_Name"] and r["Counter_Name"] == counter:
@@ -30,7 +30,7 @@ def per_launch(path, kernel, counter):
             disp.add(r.get("Dispatch_Id") or r.get("Correlation_Id") or len(disp))
     if not disp:
         raise SystemExit("no %s rows for kernel %r in %s" % (counter, kernel, path))
-    return tot / len(disp), len(disp)
+    return tot / (frames or len(disp)), len(disp)
 
 
 def main():
@@ -40,9 +40,12 @@ def main():
     ap.add_argument("fetch_csv")
     ap.add_argument("write_csv")
     ap.add_argument("--note", default="")
+    ap.add_argument("--frames", type=int, default=None,
+                    help="sum every matching dispatch and divide by this many frames (BDPT: the "
+                         "wavefront sequence of one frame is the 'launch')")
     a = ap.parse_args()
-    f_kb, nf = per_launch(a.fetch_csv, a.kernel, "FETCH_SIZE")
-    w_kb, nw = per_launch(a.write_csv, a.kernel, "WRITE_SIZE")
+    f_kb, nf = per_launch(a.fetch_csv, a.kernel, "FETCH_SIZE", a.frames)
+    w_kb, nw = per_launch(a.write_csv, a.kernel, "WRITE_SIZE", a.frames)
     entry = {"kernel": a.kernel, "fetch_size_kb": round(f_kb, 1), "write_size_kb": round(w_kb, 1),
              "bytes_per_launch": round((2.0 * f_kb + w_kb) * 1024.0),
              "correction": "bytes = (2 x FETCH_SIZE + WRITE_SIZE) x 1024 (gfx950 FETCH_SIZE halving)",
