@@ -4,6 +4,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <random>
 #include "../../toypathtracer-games101-assignment7_amd/csrc/tpt_devmath.h"
 using namespace tpt;
 int main(int argc, char** argv) {
@@ -61,5 +62,38 @@ int main(int argc, char** argv) {
         }
     }
     printf("sincos_d-products n=%ld bad=%ld\n", n5, bad5);
-    return (bad || bad2 || bad3 || bad4 || bad5) ? 1 : 0;
+    // div3_rcp (the device's shared-denominator division) against IEEE float
+    // division, with a reciprocal estimate 2^-20 off (v_rcp_f64 is much closer):
+    // random bit patterns over all finite operands, and operands built so that the
+    // exact quotient sits next to a rounding midpoint.
+    long bad6 = 0, n6 = 0;
+    {
+        std::mt19937_64 g(7);
+        std::uniform_real_distribution<double> pert(-std::ldexp(1.0, -20), std::ldexp(1.0, -20));
+        const long iters = 20000000L * 61 / (long)stride;
+        for (long i = 0; i < iters; ++i) {
+            const float x = u2f((uint32_t)g()), r = u2f((uint32_t)g());
+            if (!std::isfinite(x) || !std::isfinite(r) || r == 0.0f) continue;
+            const V3 q = div3_rcp(v3(x, -x, x), r, (1.0 / (double)r) * (1.0 + pert(g)));
+            const float w = x / r;
+            n6++;
+            if (f2u(q.x) != f2u(w) || f2u(q.y) != f2u(-x / r)) bad6++;
+        }
+        std::uniform_int_distribution<uint32_t> mant(0, (1u << 23) - 1);
+        std::uniform_int_distribution<int> ex(-60, 60);
+        for (long i = 0; i < iters / 4; ++i) {
+            const float r = std::ldexp(1.0f + mant(g) / 8388608.0f, ex(g));
+            const float q = std::ldexp(1.0f + mant(g) / 8388608.0f, ex(g));
+            const double mid = (double)q + std::ldexp(1.0, std::ilogb(q) - 24);
+            const float x0 = (float)(mid * (double)r);
+            for (int k = -2; k <= 2; ++k) {
+                const float x = u2f(f2u(x0) + k);
+                if (!std::isfinite(x)) continue;
+                n6++;
+                if (f2u(div3_rcp(v3(x, x, x), r, (1.0 / (double)r) * (1.0 + pert(g))).x) != f2u(x / r)) bad6++;
+            }
+        }
+    }
+    printf("div3_rcp n=%ld bad=%ld\n", n6, bad6);
+    return (bad || bad2 || bad3 || bad4 || bad5 || bad6) ? 1 : 0;
 }

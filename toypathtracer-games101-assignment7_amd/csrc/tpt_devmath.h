@@ -60,7 +60,34 @@ TPT_HD V3 operator*(V3 a, V3 b) { return v3(a.x * b.x, a.y * b.y, a.z * b.z); }
 TPT_HD V3 operator/(V3 a, V3 b) { return v3(a.x / b.x, a.y / b.y, a.z / b.z); }
 TPT_HD V3 operator-(V3 a) { return v3(-a.x, -a.y, -a.z); }
 TPT_HD V3 mul(V3 a, float r) { return v3(a.x * r, a.y * r, a.z * r); }   // Vector.hpp:25,48
-TPT_HD V3 divs(V3 a, float r) { return v3(a.x / r, a.y / r, a.z / r); }  // Vector.hpp:26
+
+// Three correctly rounded float quotients a.{x,y,z} / r sharing one denominator
+// (Vector.hpp:26 operator/, and Normalized's x/n, y/n, z/n), from ONE f64
+// reciprocal: y = two Newton steps from the estimate y0, then RN32(RN64(a * y)).
+// Exact: for floats a, r the quotient a/r is never a midpoint of two adjacent
+// floats and lies at least 2^-49 (relative) from every midpoint (a = m*r would need
+// a 49-bit product to have 24 significant bits), while y is within ~2^-52 of 1/r
+// once y0 is within 2^-20 (v_rcp_f64 is far closer), so RN64(a*y) is within
+// 2^-51 of a/r and rounds to the same float -- denormal results included (the
+// absolute error, < 2^-177, is below their 2^-150 midpoint spacing).  Needs r finite
+// and non-zero (the caller falls back to the plain quotient otherwise).  Checked
+// against IEEE division with a deliberately poor y0 (relative error 2^-20) on
+// random and near-midpoint operands: tests/native/devmath_check.cpp.
+TPT_HD V3 div3_rcp(V3 a, float r, double y0) {
+    const double d = (double)r;
+    double e = __builtin_fma(-d, y0, 1.0);
+    double y = __builtin_fma(y0, e, y0);
+    e = __builtin_fma(-d, y, 1.0);
+    y = __builtin_fma(y, e, y);
+    return v3((float)((double)a.x * y), (float)((double)a.y * y), (float)((double)a.z * y));
+}
+TPT_HD V3 divs(V3 a, float r) {  // Vector.hpp:26
+#if defined(__HIPCC__) && defined(__HIP_DEVICE_COMPILE__)
+    if (__builtin_expect(r != 0.0f && __builtin_fabsf(r) <= 3.40282347e+38f, 1))
+        return div3_rcp(a, r, __builtin_amdgcn_rcp((double)r));
+#endif
+    return v3(a.x / r, a.y / r, a.z / r);
+}
 
 // Vector.hpp:103-104 (see header note on the fma form)
 TPT_HD double dot3(V3 a, V3 b) {
@@ -91,7 +118,7 @@ TPT_HD double sqrt_d(double x) {
 }
 TPT_HD V3 normalized(V3 a) {  // Vector.hpp:31-34
     float n = sqrt_f(a.x * a.x + a.y * a.y + a.z * a.z);
-    return v3(a.x / n, a.y / n, a.z / n);
+    return divs(a, n);  // x / n, y / n, z / n
 }
 TPT_HD V3 normalize_len2(V3 a, float* len2) {  // Vector.hpp:36-39
     *len2 = (float)dot3(a, a);
