@@ -482,8 +482,13 @@ constexpr int kRecV = 4;  // float4 per vertex record
 struct WfState {
     float4* rec;          // n * 32 * kRecV float4
     int* cnt;             // cn | ln << 16
-    unsigned long long* np;    // strategies per pixel: (s = 0 ones: cn - 1) | (the others: cn * ln) << 32
-    unsigned long long* incl;  // inclusive scan of np (both halves at once)
+    // strategies per pixel in four classes (task runs, see tpt_bdpt_scatter_kernel):
+    //   np  = (s = 0: cn - 1) | (t > 1, s > 1: (cn - 1)(ln - 1)) << 32
+    //   np2 = (t > 1, s = 1: cn - 1) | (t = 1: ln) << 32
+    unsigned long long* np;
+    unsigned long long* incl;   // inclusive scan of np (both halves at once)
+    unsigned long long* np2;
+    unsigned long long* incl2;  // inclusive scan of np2
     int* tres;            // task -> canonical strategy index (res slot)
     unsigned long long* task;  // strategy -> pixel | t << 40 | s << 48
     float* res;           // 3 floats per strategy

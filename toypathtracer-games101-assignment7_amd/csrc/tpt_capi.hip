@@ -295,7 +295,8 @@ __global__ __launch_bounds__(kBlock, TPT_GEN_MINWAVES) void tpt_bdpt_gen_kernel(
         if (ln >= 0) {
             w.rng[k] = rs;
             w.cnt[k] = cn | (ln << 16);
-            w.np[k] = (unsigned long long)(cn - 1) | ((unsigned long long)(cn * ln) << 32);
+            w.np[k] = (unsigned long long)(cn - 1) | ((unsigned long long)((cn - 1) * (ln - 1)) << 32);
+            w.np2[k] = (unsigned long long)(cn - 1) | ((unsigned long long)ln << 32);
             nbounce += (unsigned long long)(cn + ln);
             k = -1;
         }
@@ -304,22 +305,39 @@ __global__ __launch_bounds__(kBlock, TPT_GEN_MINWAVES) void tpt_bdpt_gen_kernel(
 }
 
 
-// Canonical (t, s)-order range of pixel k's strategies and the starts of its two
-// task runs (s = 0 run in [0, n0_total), connecting run after it).
+// Task runs.  A strategy's cost depends on its class: s = 0 (emission only), and
+// for connections whether the light-side vertex is the light itself (s = 1: no BSDF
+// there) and whether the camera-side one is the camera (t = 1: no BSDF, a splat).
+// The task list holds four runs, each pixel-major in (t, s) order:
+//   [s = 0][t > 1, s > 1][t > 1, s = 1][t = 1]
+// so a wave's 64 strategies are (nearly always) of one class and take the same
+// branches through PathWeight.  Results still land in their canonical (t, s) slots.
 struct StratRange {
-    int64_t canon, b0, b1;
-    int n0, n1, ln;
+    int64_t canon;       // first canonical slot of the pixel
+    int64_t b[4];        // the pixel's start in each run (absolute task index)
+    int ln, np;          // light vertices, strategies
 };
 TPT_D StratRange strat_range(const WfState& w, int64_t k) {
-    const unsigned long long e = w.incl[k], c = w.np[k];
+    const unsigned long long e1 = w.incl[k], c1 = w.np[k], e2 = w.incl2[k], c2 = w.np2[k];
+    const unsigned long long t1 = w.incl[w.n - 1], t2 = w.incl2[w.n - 1];
+    const int64_t totA = (int64_t)(t1 & 0xffffffffull), totE = (int64_t)(t1 >> 32), totD = (int64_t)(t2 & 0xffffffffull);
+    const int64_t xA = (int64_t)(e1 & 0xffffffffull) - (int64_t)(c1 & 0xffffffffull);
+    const int64_t xE = (int64_t)(e1 >> 32) - (int64_t)(c1 >> 32);
+    const int64_t xD = (int64_t)(e2 & 0xffffffffull) - (int64_t)(c2 & 0xffffffffull);
+    const int64_t xT = (int64_t)(e2 >> 32) - (int64_t)(c2 >> 32);
     StratRange r;
-    r.n0 = (int)(c & 0xffffffffull);
-    r.n1 = (int)(c >> 32);
-    r.b0 = (int64_t)(e & 0xffffffffull) - r.n0;
-    r.b1 = (int64_t)(e >> 32) - r.n1;
-    r.canon = r.b0 + r.b1;
+    r.canon = xA + xE + xD + xT;
+    r.b[0] = xA;
+    r.b[1] = totA + xE;
+    r.b[2] = totA + totE + xD;
+    r.b[3] = totA + totE + totD + xT;
     r.ln = w.cnt[k] >> 16;
+    r.np = (int)(c1 & 0xffffffffull) + (int)(c1 >> 32) + (int)(c2 & 0xffffffffull) + (int)(c2 >> 32);
     return r;
+}
+TPT_D int64_t total_tasks(const WfState& w) {
+    const unsigned long long t1 = w.incl[w.n - 1], t2 = w.incl2[w.n - 1];
+    return (int64_t)(t1 & 0xffffffffull) + (int64_t)(t1 >> 32) + (int64_t)(t2 & 0xffffffffull) + (int64_t)(t2 >> 32);
 }
 
 __global__ __launch_bounds__(kBlock) void tpt_bdpt_scatter_kernel(WfState w, unsigned* __restrict__ queue) {
@@ -327,11 +345,14 @@ __global__ __launch_bounds__(kBlock) void tpt_bdpt_scatter_kernel(WfState w, uns
     if (k < 8) queue[k * 16] = 0;  // gen of the next iteration (same stream, after this kernel) starts its shards at 0
     if (k >= w.n) return;
     const StratRange r = strat_range(w, k);
-    const int64_t n0_total = (int64_t)(w.incl[w.n - 1] & 0xffffffffull);
-    const int np = r.n0 + r.n1;
-    for (int pi = 1; pi <= np; ++pi) {  // strategy index in (t, s) order; pi = 0 skipped
-        const int t = pi / (r.ln + 1) + 1, sl = pi % (r.ln + 1);
-        const int64_t g = sl == 0 ? r.b0 + (t - 2) : n0_total + r.b1 + (int64_t)(t - 1) * r.ln + (sl - 1);
+    const int ln = r.ln;
+    for (int pi = 1; pi <= r.np; ++pi) {  // strategy index in (t, s) order; pi = 0 skipped
+        const int t = pi / (ln + 1) + 1, sl = pi % (ln + 1);
+        int64_t g;
+        if (sl == 0) g = r.b[0] + (t - 2);
+        else if (t == 1) g = r.b[3] + (sl - 1);
+        else if (sl == 1) g = r.b[2] + (t - 2);
+        else g = r.b[1] + (int64_t)(t - 2) * (ln - 1) + (sl - 2);
         w.task[g] = (unsigned long long)k | ((unsigned long long)t << 40) | ((unsigned long long)sl << 48);
         w.tres[g] = (int)(r.canon + pi - 1);
     }
@@ -343,8 +364,7 @@ template <bool kLds>
 __global__ __launch_bounds__(kBlock, TPT_CONN_MINWAVES) void tpt_bdpt_conn_kernel(DScene s, WfState w, float* __restrict__ splat) {
     int* stk = stage_scene<kLds>(s);
     TPT_PACKET_DECL
-    const unsigned long long tot = w.incl[w.n - 1];
-    const int64_t total = (int64_t)(tot & 0xffffffffull) + (int64_t)(tot >> 32);
+    const int64_t total = total_tasks(w);
     const V3 eye = v3(s.eye[0], s.eye[1], s.eye[2]);
 #ifdef TPT_STAMPS
     Stamps st{};
@@ -402,7 +422,7 @@ __global__ __launch_bounds__(kBlock) void tpt_bdpt_fold_kernel(WfState w, float 
     const int64_t k = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (k >= w.n) return;
     const StratRange r = strat_range(w, k);
-    const int64_t b = r.canon, e = r.canon + r.n0 + r.n1;
+    const int64_t b = r.canon, e = r.canon + r.np;
     const int ln = r.ln;
     V3 res = v3s(0.0f);  // BDPT.cpp:289 `Vector3f result;`
     for (int64_t g = b + ln; g < e; ++g)  // pi = g - b + 1 > ln: t > 1 (t = 1 strategies were splatted)
@@ -529,7 +549,7 @@ int ensure_wf(tpt_ctx* c, int64_t n) {
     auto al = [](int64_t b) { return (b + 255) & ~(int64_t)255; };
     const int64_t b_rec = al(2 * kMaxLen * kRecV * n * 16), b_i = al(n * 4), b_l = al(n * 8),
                   b_own = al(n * maxs * 8), b_tres = al(n * maxs * 4), b_res = al(n * maxs * 12), b_acc = al(n * 12);
-    const int64_t per_buf = b_rec + b_i + 2 * b_l + b_own + b_tres + b_res;
+    const int64_t per_buf = b_rec + b_i + 4 * b_l + b_own + b_tres + b_res;
     const int64_t total = 2 * per_buf + b_i + b_acc;
     HIP_TRY(c, hipMalloc(&c->wf_mem, total));
     char* p = (char*)c->wf_mem;
@@ -539,6 +559,8 @@ int ensure_wf(tpt_ctx* c, int64_t n) {
         w.cnt = (int*)p; p += b_i;
         w.np = (unsigned long long*)p; p += b_l;
         w.incl = (unsigned long long*)p; p += b_l;
+        w.np2 = (unsigned long long*)p; p += b_l;
+        w.incl2 = (unsigned long long*)p; p += b_l;
         w.task = (unsigned long long*)p; p += b_own;
         w.tres = (int*)p; p += b_tres;
         w.res = (float*)p; p += b_res;
@@ -626,6 +648,9 @@ int launch(tpt_ctx* c, int mode, int spp, int64_t begin, int64_t stride, int64_t
             HIP_TRY(c, rocprim::inclusive_scan(c->scan_tmp, bytes, w.np, w.incl, (size_t)count,
                                                rocprim::plus<unsigned long long>(),
                                                c->stream));
+            bytes = c->scan_bytes;
+            HIP_TRY(c, rocprim::inclusive_scan(c->scan_tmp, bytes, w.np2, w.incl2, (size_t)count,
+                                               rocprim::plus<unsigned long long>(), c->stream));
             hipLaunchKernelGGL(tpt_bdpt_scatter_kernel, dim3(pblocks), dim3(kBlock), 0, c->stream, w, c->queue);
             HIP_TRY(c, hipEventRecord(c->ev_gen[b], c->stream));
             HIP_TRY(c, hipStreamWaitEvent(s2, c->ev_gen[b], 0));
