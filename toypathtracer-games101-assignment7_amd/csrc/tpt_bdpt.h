@@ -584,6 +584,91 @@ TPT_D bool light_start_rec(const DScene& s, const WfState& w, int64_t k, BVert& 
     return !(pdf1 == 0.0f && it.type == T_BG);
 }
 
+// One generation step of a lane's sample, for the persistent gen kernel: either
+// GenerateLightPath's start (phase 1: light vertex l0 and the first bounce l1,
+// BDPT.cpp:61-90) or one iteration of FillPathUsingRussianRoulette's loop
+// (extend_rec).  Both end in ONE closest-hit query, so a wave whose lanes are in
+// different phases traces a single query instead of one per phase (the light start
+// used to run beside every extension step).  Same draws, vertices and float ops as
+// light_start_rec / extend_rec.  Returns false when the current subpath has ended:
+// its vertex count is then i + 1.
+template <bool kPacket>
+TPT_D bool gen_step(const DScene& s, const WfState& w, int64_t k, int& phase, BVert& prev, BVert& cur, int& i,
+                    uint32_t& rs, Packet pk, int* stk) {
+    const bool start = phase == 1;
+    bool go = true;
+    Ray ray;
+    int cl = TPT_CULL_BACK;
+    float sr = 0.0f;
+    if (start) {
+        const DObj lo = s.objs[s.emitters[0]];
+        V3 pc, pn;
+        int pp;
+        object_sample(s, lo, pc, pn, pp, rs);
+        BVert l0;
+        l0.x = pc; l0.N = pn; l0.type = T_LIGHT; l0.prim = pp; l0.mat = lo.mat;
+        l0.pdf = lo.pdf;
+        l0.alpha = divs(load_mat(s, lo.mat).em, l0.pdf);
+        l0.q1 = l0.q8 = 0.0f;
+        float pdf1;
+        const V3 wi = cosine_sample(pn, pdf1, rs);
+        const float ct = (float)dot3(l0.N, wi);
+        sr = safe_div(pdf1, ct);
+        ray = make_ray(l0.x, wi);
+        rec_store(w, kMaxLen, k, l0);
+        cur = l0;
+    } else {
+        go = !(i >= kMaxLen - 1 || cur.type == T_BG);
+        if (go) {
+            const V3 wo = normalized(prev.x - cur.x);
+            float raw;
+            const V3 wi = mat_sample(load_mat(s, cur.mat), wo, cur.N, &raw, rs);
+            const float rr = i > 4 ? .8f : 1.f;
+            go = !(rng_float(rs) > rr);
+            if (go) {
+                const float ct = (float)dabs_(dot3(cur.N, wi));
+                sr = safe_div(raw, ct);
+                ray = make_ray(cur.x, wi);
+                cl = dot3(cur.N, wi) > 0.0f ? TPT_CULL_BACK : TPT_CULL_FRONT;
+            }
+        }
+    }
+    if (!go) return false;
+    PTV it = kPacket ? scene_intersect_packet(s, ray, cl, pk) : scene_intersect(s, ray, cl, stk);
+    const float pdf = srpdf_to_area(sr, cur.type, cur.x, cur.N, it.type, it.x, it.N);
+    BVert nx;
+    nx.x = it.x; nx.N = it.N; nx.type = it.type; nx.prim = it.prim;
+    nx.mat = it.prim >= 0 ? prim_mat(s, it.prim) : -1;
+    nx.q1 = nx.q8 = 0.0f;
+    if (start) {
+        nx.pdf = pdf;
+        nx.alpha = v3s(0.0f);  // fresh InternalPathVertex (BDPT.hpp:19)
+        if (sr != 0.0f) nx.alpha = safe_div(cur.alpha, sr);
+        rec_store(w, kMaxLen + 1, k, nx);
+        prev = cur;
+        cur = nx;
+        i = 1;
+        phase = 2;
+        return !(sr == 0.0f && it.type == T_BG);
+    }
+    if (pdf == 0.0f) return false;
+    const V3 wo = normalized(prev.x - cur.x);
+    const Mat m = load_mat(s, cur.mat);
+    const float rr = i > 4 ? .8f : 1.f;
+    const V3 bsdf = eval_bsdf(m, wo, ray.d, cur.N, false);
+    nx.pdf = pdf * rr;
+    nx.alpha = divs(cur.alpha * safe_div(bsdf, sr), rr);
+    const int base = phase == 0 ? 0 : kMaxLen;
+    rec_store(w, base + i + 1, k, nx);
+    // path_rev for j = i - 1: Append(P[j]) after last = P[i], Pre = P[i+1]
+    const float rev = append_pdf(s, cur.type, cur.mat, cur.x, cur.N, nx.x, prev.type, prev.x, prev.N);
+    rec_store_q(w, base + i - 1, k, safe_div(rev * 1.f, prev.pdf), safe_div(rev * .8f, prev.pdf));
+    prev = cur;
+    cur = nx;
+    ++i;
+    return true;
+}
+
 struct GlobPaths {  // one pixel's paths in the HBM records
     const float4* rec;  // this pixel's 32 vertex records
     TPT_D BVert load(int slot) const {

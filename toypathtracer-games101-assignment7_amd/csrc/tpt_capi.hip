@@ -273,18 +273,7 @@ __global__ __launch_bounds__(kBlock, TPT_GEN_MINWAVES) void tpt_bdpt_gen_kernel(
         if (__ballot(k >= 0) == 0) break;  // every lane idle and its shard drained
         if (k < 0) continue;
         int ln = -1;  // >= 0: the pixel's sample is complete
-        if (phase == 1) {
-            BVert l0, l1;
-            if (light_start_rec<TPT_GEN_PACKET>(s, w, k, l0, l1, rs, pk, stk)) {
-                prev = l0;
-                cur = l1;
-                i = 1;
-                phase = 2;
-            } else {
-                ln = 2;
-            }
-        }
-        if (ln < 0 && !extend_rec<TPT_GEN_PACKET>(s, w, k, phase == 0 ? 0 : kMaxLen, prev, cur, i, rs, pk, stk)) {
+        if (!gen_step<TPT_GEN_PACKET>(s, w, k, phase, prev, cur, i, rs, pk, stk)) {
             if (phase == 0) {
                 cn = i + 1;
                 phase = 1;
