@@ -43,7 +43,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--mode", choices=("pt", "bdpt"), default="pt")
+    ap.add_argument("--mode", choices=("pt", "bdpt", "pti"), default="pt",
+                    help="pti: PathTrace with the indirect bounce on (TPT_MODE_PT_INDIRECT, not a BASELINE config)")
     ap.add_argument("--scene", default="standard")
     ap.add_argument("--spp", type=int, default=None, help="default 1024 (PT) / 256 (BDPT), BASELINE configs 1-2")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
@@ -67,9 +68,11 @@ def cpu_baseline(mode, scene, threads):
     """Bounded CPU sample on this host (about 10-30 s of CPU work)."""
     import numpy as np
     from oracle_bind import Oracle, Reference, ref_available
-    spp = 64 if mode == "pt" else 2
-    m = 0 if mode == "pt" else 1
-    if ref_available():
+    spp = {"pt": 64, "pti": 16}.get(mode, 2)
+    m = {"pt": 0, "bdpt": 1, "pti": 2}[mode]
+    # Renderer::Render has no switch for the indirect bounce: for "pti" the baseline is
+    # the restatement (bit-exact to the reference built without PathTracer.cpp:109)
+    if ref_available() and mode != "pti":
         # the reference prints its progress lines from C++ (fd 1): keep them off the
         # bench's one-JSON-line stdout
         sys.stdout.flush()
@@ -105,7 +108,7 @@ def main():
     import torch
 
     mode = a.mode
-    spp = a.spp or (1024 if mode == "pt" else 256)
+    spp = a.spp or (256 if mode == "bdpt" else 1024)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -127,7 +130,7 @@ def main():
     ctx.upload(preset)
     W, H = ctx.width, ctx.height
     fb = torch.zeros(2, H * W * 3, dtype=torch.float32, device="cuda")  # rgb + splat, one reduce buffer
-    m = pytpt.MODE_PT if mode == "pt" else pytpt.MODE_BDPT
+    m = {"pt": pytpt.MODE_PT, "bdpt": pytpt.MODE_BDPT, "pti": pytpt.MODE_PT_INDIRECT}[mode]
     shard_begin, shard_stride = sharding.shard(rank, world)  # Renderer.cpp:38 interleave
 
     def step():
@@ -165,7 +168,7 @@ def main():
         roofline = {"bound": "hbm", "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
                     "traffic": a.traffic_bytes if a.traffic_bytes is not None else pmc_traffic(a.scene, mode),
-                    "kernel": "tpt_pt_kernel" if mode == "pt" else "bdpt wavefront sequence (gen+scan+scatter+conn+fold) x spp", "kernel_ms": round(kernel_ms, 3),
+                    "kernel": {"pt": "tpt_pt_kernel", "pti": "tpt_pti_kernel"}.get(mode, "bdpt wavefront sequence (gen+scan+scatter+conn+fold) x spp"), "kernel_ms": round(kernel_ms, 3),
                     "bytes_per_sample_alg": b_alg, "samples_per_launch": shard_samples,
                     "note": "algorithmic scene-fetch bytes (SURVEY 8d); scene is L2-resident, real bound is VALU"}
         cpu = None

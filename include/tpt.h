@@ -61,6 +61,10 @@ extern "C" {
 /* render modes */
 #define TPT_MODE_PT 0    /* PathTrace, PathTracer.cpp:44 */
 #define TPT_MODE_BDPT 1  /* BDPT, BDPT.cpp:282 */
+/* PathTrace with the indirect bounce enabled: PathTracer.cpp:44-134 without the
+ * `break` at :109 (dead code at HEAD).  Off by default: no
+ * reference entry point selects it, and it changes results against HEAD. */
+#define TPT_MODE_PT_INDIRECT 2
 
 /* Material (Material.hpp:15-44).  `rough` is the already-converted roughness
  * (Material::SetSmoothness -> SmoothnessToRoughenss, GGX.hpp:38-40). */
@@ -102,7 +106,7 @@ typedef struct tpt_scene_desc {
 
 typedef struct tpt_render_params {
     int32_t spp;                  /* samples per pixel (Renderer.cpp:43) */
-    int32_t mode;                 /* TPT_MODE_PT | TPT_MODE_BDPT */
+    int32_t mode;                 /* TPT_MODE_PT | TPT_MODE_BDPT | TPT_MODE_PT_INDIRECT */
     int64_t pixel_begin;          /* first pixel of this shard (Renderer.cpp:38 `i = off`) */
     int64_t pixel_stride;         /* shard stride (Renderer.cpp:38 `i += j`); 1 = all pixels */
     int32_t flags;                /* reserved, 0 */

@@ -107,6 +107,7 @@ struct RenderOptions {
     int gpus = 1;                // >1: pixel-sharded multi-GPU (one process per GPU: see bench.py)
     std::string float_dump;      // optional raw fp32 W*H*3 dump (parity artefact)
     bool quiet = false;
+    bool pt_indirect = false;    // PathTrace with the indirect bounce (TPT_MODE_PT_INDIRECT); off by default
 };
 
 class Renderer {

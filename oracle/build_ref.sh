@@ -9,6 +9,8 @@
 #     it is compiled from a one-token on-the-fly sed of the original file
 #     (`auto& lastVertex` -> `auto lastVertex`; PathVertex is a {path*,index}
 #     handle so behaviour is unchanged).  No patched copy is written anywhere.
+#   * PathTracer.cpp is compiled a second time with the HEAD `break` (:109)
+#     removed, as PathTraceIndirect (TPT_MODE_PT_INDIRECT's reference);
 #   * main.cpp is not linked (the harness provides the scene presets).
 set -euo pipefail
 REF=${REF:-/root/reference}
@@ -25,6 +27,13 @@ for s in $SRCS; do
 done
 sed 's/auto& lastVertex = this->operator\[\](count - 1);/auto lastVertex = this->operator[](count - 1);/' "$REF/BDPT.cpp" \
   | $CXX $FLAGS -x c++ -c - -o "$OUT/obj/BDPT.o" & pids+=($!)
+# TPT_MODE_PT_INDIRECT's reference: PathTracer.cpp once more, with the `break` at
+# :109 (the end of the HEAD iteration) dropped and the function renamed
+# PathTraceIndirect, again through a sed pipe.  Refuse if :109 is not that line.
+sed -n '109p' "$REF/PathTracer.cpp" | grep -qx '[[:space:]]*break;[[:space:]]*' \
+  || { echo "build_ref: PathTracer.cpp:109 is not the HEAD break" >&2; exit 1; }
+sed -e '109s/break;//' -e 's/^Vector3f PathTrace(/Vector3f PathTraceIndirect(/' "$REF/PathTracer.cpp" \
+  | $CXX $FLAGS -x c++ -c - -o "$OUT/obj/PathTracerIndirect.o" & pids+=($!)
 $CXX $FLAGS -c "$HERE/ref_harness.cpp" -o "$OUT/obj/ref_harness.o" & pids+=($!)
 for p in "${pids[@]}"; do wait "$p"; done
 WRAP=_Z19SaveFloatImageToJpgSt6vectorI8Vector3fSaIS0_EEiiNSt7__cxx1112basic_stringIcSt11char_traitsIcESaIcEEE

@@ -48,6 +48,10 @@ void wrapped_save(std::vector<Vector3f> fb, int w, int h, std::string) {
 // Renderer.cpp:29 -- FillBufferThread reads the scene through this global.
 extern const Scene* curScene;
 
+// PathTracer.cpp compiled a second time without the HEAD `break` (:109), see
+// oracle/build_ref.sh: the reference for TPT_MODE_PT_INDIRECT.
+Vector3f PathTraceIndirect(const Scene* scene, const Ray& ray, int& outBounces);
+
 namespace {
 struct Preset {
     Scene* scene = nullptr;
@@ -135,7 +139,8 @@ void ref_render(int spp, int threads, int bdpt, float* out_rgb) {
     g_capture = nullptr;
 }
 
-// Per-pixel replay (Renderer.cpp:38-60) for an arbitrary pixel subset.  `splat`
+// Per-pixel replay (Renderer.cpp:38-60) for an arbitrary pixel subset; mode
+// `bdpt`: 0 PathTrace, 1 BDPT, 2 PathTraceIndirect.  `splat`
 // (W*H*3, may be null) receives the t=1 light-tracing splats of those pixels,
 // already scaled by 1/spp as in Renderer.cpp:58-60.  `bounces` (may be null)
 // receives the per-pixel outBounces sum.
@@ -152,7 +157,8 @@ void ref_trace_pixels(int bdpt, int spp, const int64_t* pix, int n, float* out_r
         for (int ispp = 0; ispp < spp; ++ispp) {
             Vector3f dir = PixelPosToRay(xPixel, yPixel, s->width, s->height, scale);
             int b = 0;
-            if (bdpt) acc += (1.0f / spp) * BDPT(s, Ray(s->eyePos, dir), b, &emission[0]);
+            if (bdpt == 1) acc += (1.0f / spp) * BDPT(s, Ray(s->eyePos, dir), b, &emission[0]);
+            else if (bdpt == 2) acc += (1.0f / spp) * PathTraceIndirect(s, Ray(s->eyePos, dir), b);
             else acc += (1.0f / spp) * PathTrace(s, Ray(s->eyePos, dir), b);
             nb += b;
         }

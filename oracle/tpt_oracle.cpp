@@ -737,6 +737,57 @@ static V3 path_trace(const Scene& sc, const Ray& ray, int& bounces) {
     return result;
 }
 
+// PathTracer.cpp:44-134 with the `break` at :109 removed (TPT_MODE_PT_INDIRECT,
+// the reference's dead indirect-bounce code re-enabled; its
+// oracle is the reference built with that one line dropped, oracle/build_ref.sh).
+static V3 path_trace_indirect(const Scene& sc, const Ray& ray, int& bounces) {
+    bounces = 0;
+    Ray cur = ray;
+    V3 alpha(1.0f), result(0.0f);
+    bool explicit_light = false, flip = false;
+    for (;;) {
+        if (alpha.x == 0.0f && alpha.y == 0.0f && alpha.z == 0.0f) break;               // :54-55
+        PTV it = sc.intersect(cur, flip ? TPT_CULL_FRONT : TPT_CULL_BACK);             // :56
+        if (it.type == T_BG) break;                                                    // :58-62
+        const Material& m = sc.mat_of(it.prim);
+        if (m.has_emission() && !explicit_light) result = result + alpha * m.emission;  // :64-68
+        V3 x = it.x, wo = -cur.d, n = it.N;
+        float pdf_b;
+        V3 wib = mat_sample(m, wo, n, &pdf_b);                                         // :76
+        explicit_light = true;                                                         // :80
+        for (int L : sc.emitters) {                                                    // :82-106
+            float pll, pbl, plb;
+            V3 wil = light_sample(sc, L, x, &pll);
+            plb = mat_pdf(m, wo, n, wil);
+            pbl = light_pdf(sc, L, x, wib);
+            V3 ev(0.0f);
+            if (pdf_b + pbl > 0.0f) {
+                Hit h = sc.object_hit(L, Ray(x, wib), TPT_CULL_BACK);
+                if (h.happened && !sc.shadow(h.coords, x))
+                    ev = ev + divs(eval_bsdf(m, wo, wib, n, true), EPS + pdf_b + pbl);
+            }
+            if (pll + plb > 0.0f) {
+                Hit h = sc.object_hit(L, Ray(x, wil), TPT_CULL_BACK);
+                if (!sc.shadow(h.coords, x))
+                    ev = ev + divs(eval_bsdf(m, wo, wil, n, true), EPS + pll + plb);
+            }
+            result = result + alpha * ev * sc.mats[sc.objects[L].mat].emission;
+        }
+        V3 weight(0.0f);                                                               // :111-114
+        if (pdf_b > 0.0f) weight = divs(eval_bsdf(m, wo, wib, n, true), EPS + pdf_b);
+        cur = Ray(x, wib);                                                             // :116
+        flip = dot(n, wib) < 0.0f;                                                     // :117-120
+        const bool rr = bounces > 4;                                                   // :122-131
+        if (!rr || rand_float() < 0.8f) {
+            alpha = divs(alpha * weight, rr ? 0.8f : 1.0f);
+            bounces += 1;
+            continue;
+        }
+        break;
+    }
+    return result;
+}
+
 // --------------------------------------------------------------- BDPT ----
 // BDPT.hpp:8-9, BDPT.cpp:7-8
 static const int MAXLEN = 16;
@@ -1155,7 +1206,9 @@ static void trace_pixel(const Scene& sc, float scale, int mode, int spp, int64_t
     for (int s = 0; s < spp; ++s) {
         V3 dir = pixel_ray(px, py, sc.width, sc.height, scale);
         int b = 0;
-        V3 L = mode == TPT_MODE_BDPT ? bdpt(sc, scale, Ray(sc.eye, dir), b, splat) : path_trace(sc, Ray(sc.eye, dir), b);
+        V3 L = mode == TPT_MODE_BDPT          ? bdpt(sc, scale, Ray(sc.eye, dir), b, splat)
+               : mode == TPT_MODE_PT_INDIRECT ? path_trace_indirect(sc, Ray(sc.eye, dir), b)
+                                              : path_trace(sc, Ray(sc.eye, dir), b);
         acc = acc + mul(L, 1.0f / spp);
         nb += b;
     }

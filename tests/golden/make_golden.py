@@ -13,6 +13,11 @@ Contents (all float32 unless noted):
                         (+ BDPT t=1 splats of those pixels as a sparse list)
   image_standard.npz    real Renderer::Render framebuffers: PT 16 spp (8x8 block
                         means + a 64x64 full-res crop), BDPT 2 spp -j1 (same)
+  pt_indirect.npz       TPT_MODE_PT_INDIRECT: per-pixel replay through the reference's
+                        PathTrace compiled without the `break` at PathTracer.cpp:109
+                        (oracle/build_ref.sh), spp 1 and 8, radiance + outBounces sums
+
+    python tests/golden/make_golden.py indirect   # only pt_indirect.npz
 """
 import os
 import sys
@@ -89,9 +94,23 @@ def ray_set(rng, n):
     return np.concatenate([o, d.astype(np.float32)], 1).astype(np.float32)
 
 
+def indirect():
+    out = {}
+    for p in PRESETS:
+        R = Reference(p)
+        pix = pixel_set(101 + PRESETS.index(p), 1024)
+        out[p + "_pix"] = pix
+        out[p + "_spp1"], _, out[p + "_spp1_bounces"] = R.trace_pixels(2, 1, pix)
+        out[p + "_spp8"], _, out[p + "_spp8_bounces"] = R.trace_pixels(2, 8, pix)
+    np.savez_compressed(os.path.join(HERE, "pt_indirect.npz"), **out)
+    print("pt_indirect done", flush=True)
+
+
 def main():
     if not ref_available():
         sys.exit("oracle/_ref/libref.so missing: run oracle/build_ref.sh first")
+    if sys.argv[1:] == ["indirect"]:
+        return indirect()
     rng = np.random.default_rng(20261015)
     R = Reference("standard")
 
@@ -137,6 +156,7 @@ def main():
     np.savez_compressed(os.path.join(HERE, "image_standard.npz"), pt16_blocks=blocks(img_pt),
                         pt16_crop=img_pt[360:424, 360:424], bdpt2_blocks=blocks(img_bd),
                         bdpt2_crop=img_bd[360:424, 360:424], crop_origin=np.array([360, 360]))
+    indirect()
     print("done")
 
 

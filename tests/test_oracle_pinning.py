@@ -96,3 +96,26 @@ def test_live_against_reference(preset):
     a = o.trace_pixels(1, 2, pix[:400], want_splat=True)
     b = R.trace_pixels(1, 2, pix[:400], want_splat=True)
     assert eq_bits(a[0], b[0]) and eq_bits(a[1], b[1]) and np.array_equal(a[2], b[2])
+
+
+@pytest.mark.parametrize("preset", PRESETS)
+def test_pixels_pt_indirect(preset):
+    """TPT_MODE_PT_INDIRECT (PathTrace without the HEAD `break`, PathTracer.cpp:109):
+    radiance and outBounces sums against the sed-built reference's fixtures."""
+    g = golden("pt_indirect.npz")
+    o = Oracle(preset)
+    pix = g[preset + "_pix"]
+    for spp in (1, 8):
+        rgb, _, b = o.trace_pixels(2, spp, pix)
+        assert eq_bits(rgb, g["%s_spp%d" % (preset, spp)])
+        assert np.array_equal(b, g["%s_spp%d_bounces" % (preset, spp)])
+
+
+@pytest.mark.skipif(not ref_available(), reason="oracle/_ref/libref.so not built")
+@pytest.mark.parametrize("preset", ["standard", "refractive_ball", "silver"])
+def test_live_indirect_against_reference(preset):
+    rng = np.random.default_rng(17 + len(preset))
+    pix = np.sort(rng.choice(784 * 784, 2000, replace=False))
+    R, o = Reference(preset), Oracle(preset)
+    a, b = o.trace_pixels(2, 8, pix), R.trace_pixels(2, 8, pix)
+    assert eq_bits(a[0], b[0]) and np.array_equal(a[2], b[2])

@@ -44,8 +44,9 @@ TPT_D int* stage_scene(DScene& s) {
     int* stk = reinterpret_cast<int*>(tpt_smem) + threadIdx.x;
     if (kLds) {
         unsigned char* base = tpt_smem + (size_t)s.max_stack * kBlock * sizeof(int);
-        const int nb = s.nnodes * (int)sizeof(DNode), tb = s.ntri * (int)sizeof(DTri),
-                  qb = s.nqnodes * (int)sizeof(DQNode), mb = s.nmats * (int)sizeof(DMat);
+        const bool full = s.lds_full != 0;  // else only the flat-query arrays (+ ftris at the end)
+        const int nb = full ? s.nnodes * (int)sizeof(DNode) : 0, tb = full ? s.ntri * (int)sizeof(DTri) : 0,
+                  qb = full ? s.nqnodes * (int)sizeof(DQNode) : 0, mb = s.nmats * (int)sizeof(DMat);
         const uint4* gn = reinterpret_cast<const uint4*>(s.tnodes);
         const uint4* gt = reinterpret_cast<const uint4*>(s.tris);
         const uint4* gq = reinterpret_cast<const uint4*>(s.qnodes);
@@ -66,13 +67,22 @@ TPT_D int* stage_scene(DScene& s) {
         const uint4* gg = reinterpret_cast<const uint4*>(s.groups);
         uint4* lg = reinterpret_cast<uint4*>(base + go);
         for (int i = threadIdx.x; i < gb / 16; i += kBlock) lg[i] = gg[i];
+        const int fo = go + gb, fb = full ? 0 : s.nleaf * (int)sizeof(DTri);
+        const uint4* gf = reinterpret_cast<const uint4*>(s.ftris);
+        uint4* lf = reinterpret_cast<uint4*>(base + fo);
+        for (int i = threadIdx.x; i < fb / 16; i += kBlock) lf[i] = gf[i];
         __syncthreads();
         s.leaves = reinterpret_cast<const DNode*>(base + lo);
         s.groups = reinterpret_cast<const DNode*>(base + go);
-        s.tnodes = reinterpret_cast<const DNode*>(base);  // the binary `nodes` stay in L1/L2 (light sampling)
-        s.tris = reinterpret_cast<const DTri*>(base + nb);
-        s.qnodes = reinterpret_cast<const DQNode*>(base + nb + tb);
         s.mats = reinterpret_cast<const DMat*>(base + nb + tb + qb);
+        if (full) {
+            s.tnodes = reinterpret_cast<const DNode*>(base);  // the binary `nodes` stay in L1/L2 (light sampling)
+            s.tris = reinterpret_cast<const DTri*>(base + nb);
+            s.qnodes = reinterpret_cast<const DQNode*>(base + nb + tb);
+            s.ftris = s.tris;
+        } else {
+            s.ftris = reinterpret_cast<const DTri*>(base + fo);
+        }
     }
     return stk;
 }
@@ -173,6 +183,72 @@ __global__ __launch_bounds__(kBlock, TPT_PT_MINWAVES) void tpt_pt_kernel(DScene 
         out[3 * row + 1] = acc.y;
         out[3 * row + 2] = acc.z;
     }
+}
+
+#ifndef TPT_PTI_MINWAVES
+#define TPT_PTI_MINWAVES 4
+#endif
+// Generous bound on one path's bounces so that every lane provably leaves its loop.
+// A path continues past bounce 5 only on a draw < 0.8 (PathTracer.cpp:122-123); the
+// longest run of such draws in XorShift32's whole period is ~100, so the bound is
+// never reached and results are the reference's.
+constexpr int kPtiMaxBounces = 1 << 16;
+
+// TPT_MODE_PT_INDIRECT (Renderer.cpp:38-52 with PathTrace minus the :109 `break`).
+// Draws per sample depend on the geometry the path meets, so a pixel's stream is
+// one lane.  The lane runs its spp samples back to back as ONE loop of bounces: a
+// sample that ends (miss, alpha == 0, Russian roulette) is folded into the pixel and
+// the next sample starts in the same iteration, so lanes of a wave never wait for
+// one another's long paths until the pixel's last sample (per-lane regeneration,
+// in registers).
+template <bool kLds>
+__global__ __launch_bounds__(kBlock, TPT_PTI_MINWAVES) void tpt_pti_kernel(DScene s, int spp, int64_t begin,
+                                                                          int64_t stride, int64_t count,
+                                                                          const int64_t* __restrict__ list,
+                                                                          float* __restrict__ out,
+                                                                          unsigned long long* __restrict__ bounces) {
+    int* stk = stage_scene<kLds>(s);
+    TPT_PACKET_DECL
+    const int64_t k = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const bool on = k < count;
+    const int64_t i = on ? (list ? list[k] : begin + k * stride) : 0;
+    const V3 eye = v3(s.eye[0], s.eye[1], s.eye[2]);
+    const V3 dir = pixel_ray((int)(i % s.width), (int)(i / s.width), s.width, s.height, s.scale);
+    const float inv = 1.0f / spp;
+    uint32_t rs = (uint32_t)((int)i + 1);  // ResetRandom(i + 1), Renderer.cpp:42
+    V3 acc = v3s(0.0f);
+    PtiPath p;
+    p.r = make_ray(eye, dir);
+    p.alpha = v3s(1.0f);
+    p.res = v3s(0.0f);
+    p.nb = 0;
+    p.flip = false;
+    unsigned long long nbt = 0;
+    for (int j = on ? 0 : spp; j < spp;) {
+        bool live = !(p.alpha.x == 0.0f && p.alpha.y == 0.0f && p.alpha.z == 0.0f) && p.nb < kPtiMaxBounces;  // :54-55
+        if (live) {
+            const PTV v = scene_intersect(s, p.r, p.flip ? TPT_CULL_FRONT : TPT_CULL_BACK, stk);  // :56
+            live = v.type != T_BG && pti_step(s, v, p, rs, stk, pk);                              // :58-131
+        }
+        if (!live) {
+            acc = acc + mul(p.res, inv);  // Renderer.cpp:49 `fb[i] += (1.0f / spp) * L`
+            nbt += (unsigned long long)p.nb;
+            ++j;
+            p.r = make_ray(eye, dir);
+            p.alpha = v3s(1.0f);
+            p.res = v3s(0.0f);
+            p.nb = 0;
+            p.flip = false;
+        }
+    }
+    if (on) {
+        const int64_t row = list ? k : i;
+        out[3 * row + 0] = acc.x;
+        out[3 * row + 1] = acc.y;
+        out[3 * row + 2] = acc.z;
+    }
+    for (int o = 32; o >= 1; o >>= 1) nbt += __shfl_xor(nbt, o);
+    if (lane_id() == 0) atomicAdd(bounces, nbt);
 }
 
 // BDPT: Renderer.cpp:38-52 + :58-60 for TPT_MODE_BDPT.  t=1 strategies splat into
@@ -394,7 +470,7 @@ __global__ __launch_bounds__(kBlock, TPT_CONN_MINWAVES) void tpt_bdpt_conn_kerne
             }
         }
         // t = 1: DrawToImage of the light vertex (BDPT.cpp:303-305), whole wave
-        if (splat) splat_wave(s, sp, lx, eye, v, splat);
+        if (splat && !(s.dbg & 1024)) splat_wave(s, sp, lx, eye, v, splat);  // 1024: profiling ablation
         TPT_STAMP(st, 7);
     }
 #ifdef TPT_STAMPS
@@ -590,6 +666,13 @@ int launch(tpt_ctx* c, int mode, int spp, int64_t begin, int64_t stride, int64_t
         else
             hipLaunchKernelGGL(tpt_pt_kernel<false>, dim3((unsigned)qblocks), dim3(kBlock), pshmem, c->stream, c->ds,
                                spp, begin, stride, count, dlist, drows, Q);
+    } else if (mode == TPT_MODE_PT_INDIRECT) {
+        if (lds)
+            hipLaunchKernelGGL(tpt_pti_kernel<true>, dim3((unsigned)blocks), dim3(kBlock), shmem, c->stream, c->ds, spp,
+                               begin, stride, count, dlist, drows, c->counters);
+        else
+            hipLaunchKernelGGL(tpt_pti_kernel<false>, dim3((unsigned)blocks), dim3(kBlock), shmem, c->stream, c->ds,
+                               spp, begin, stride, count, dlist, drows, c->counters);
     } else if (!c->bdpt_mono) {
         int rc = ensure_wf(c, count);
         if (rc) return rc;
@@ -754,7 +837,8 @@ int check_render_args(tpt_ctx* c, int spp, int mode) {
     if (!c) return TPT_E_INVALID;
     if (!c->has_scene) return fail(c, TPT_E_NOSCENE, "no scene uploaded");
     if (spp <= 0) return fail(c, TPT_E_INVALID, "spp must be positive");
-    if (mode != TPT_MODE_PT && mode != TPT_MODE_BDPT) return fail(c, TPT_E_INVALID, "unknown mode");
+    if (mode != TPT_MODE_PT && mode != TPT_MODE_BDPT && mode != TPT_MODE_PT_INDIRECT)
+        return fail(c, TPT_E_INVALID, "unknown mode");
     if (mode == TPT_MODE_BDPT && c->hs.emitters.empty())
         return fail(c, TPT_E_INVALID, "BDPT needs an emitter (BDPT.cpp:287 uses m_emissionObjects[0])");
     return TPT_OK;
@@ -832,12 +916,46 @@ int tpt_upload_scene(tpt_ctx* c, const tpt_scene_desc* d) {
         return fail(c, TPT_E_UNSUPPORTED, "BVH deeper than the LDS traversal stack (" + std::to_string(hs.max_stack) +
                                               ", " + std::to_string(hs.q_stack) + ")");
     if (hs.nodes.size() > (size_t)0x7fffffff) return fail(c, TPT_E_UNSUPPORTED, "too many BVH nodes");
+    // LDS staging (stage_scene): every array the traversals read when it all fits in
+    // 64 KB (the Cornell presets, ~8 KB: lds_full), else only the flat-query arrays --
+    // materials, leaves, groups and the flat leaves' triangles (the bunny scene,
+    // ~2 KB) -- with the trees read through L2.  leaves[j].b indexes the triangle
+    // array flat queries read: tris itself (full) or ftris (flat-only).
+    const char* no = std::getenv("TPT_NO_LDS");
+    const bool no_lds = no && no[0] == '1';
+    const size_t mats16 = (hs.mats.size() * sizeof(DMat) + 15) & ~(size_t)15;
+    const size_t lg = (hs.leaves.size() + hs.groups.size()) * sizeof(DNode);
+    const size_t full_b = hs.nodes.size() * sizeof(DNode) + hs.tris.size() * sizeof(DTri) + mats16 +
+                          hs.qnodes.size() * sizeof(DQNode) + lg;
+    const size_t flat_b = mats16 + lg + hs.leaves.size() * sizeof(DTri);
+    int lds_full = 0;
+    size_t lds_b = 0;
+    if (!no_lds && full_b <= 64 * 1024) {
+        lds_full = 1;
+        lds_b = full_b;
+    } else if (!no_lds && hs.leaves.size() <= (size_t)kFlatMaxLeaves && flat_b <= 64 * 1024) {
+        lds_b = flat_b;
+    }
+    hs.ftris.clear();
+    for (size_t j = 0; j < hs.leaves.size(); ++j) {
+        DNode& l = hs.leaves[j];
+        const int prim = -1 - l.a;
+        const bool tri = prim < (int)hs.tris.size();
+        if (lds_full) {
+            l.b = tri ? prim : 0;
+        } else {
+            l.b = (int)j;
+            DTri t;
+            std::memset(&t, 0, sizeof(t));
+            hs.ftris.push_back(tri ? hs.tris[prim] : t);  // a sphere leaf's slot is unused
+        }
+    }
     std::vector<char> blob;
     size_t o_nodes = push_array(blob, hs.nodes), o_area = push_array(blob, hs.node_area),
            o_tris = push_array(blob, hs.tris), o_trix = push_array(blob, hs.trix), o_sph = push_array(blob, hs.sph),
            o_mats = push_array(blob, hs.mats), o_objs = push_array(blob, hs.objs),
            o_em = push_array(blob, hs.emitters), o_q = push_array(blob, hs.qnodes), o_t = push_array(blob, hs.tnodes),
-           o_lf = push_array(blob, hs.leaves), o_gr = push_array(blob, hs.groups);
+           o_lf = push_array(blob, hs.leaves), o_gr = push_array(blob, hs.groups), o_ft = push_array(blob, hs.ftris);
     if (c->blob) { (void)hipFree(c->blob); c->blob = nullptr; }
     HIP_TRY(c, hipMalloc(&c->blob, blob.size()));
     HIP_TRY(c, hipMemcpy(c->blob, blob.data(), blob.size(), hipMemcpyHostToDevice));
@@ -858,6 +976,8 @@ int tpt_upload_scene(tpt_ctx* c, const tpt_scene_desc* d) {
     ds.nleaf = (int)hs.leaves.size();
     ds.groups = (const DNode*)(b + o_gr);
     ds.ngroup = (int)hs.groups.size();
+    ds.ftris = lds_full ? ds.tris : (const DTri*)(b + o_ft);
+    ds.lds_full = lds_full;
     ds.nqnodes = (int)hs.qnodes.size();
     ds.nmats = (int)hs.mats.size();
     ds.n_emitters = (int)hs.emitters.size();
@@ -876,14 +996,8 @@ int tpt_upload_scene(tpt_ctx* c, const tpt_scene_desc* d) {
     // walk (TPT_LANE_SHADOW == 1, A/B builds) keeps an LDS stack.
     ds.max_stack = TPT_LANE_SHADOW == 1 ? hs.max_stack : 0;
     ds.q_stack = TPT_LANE_SHADOW == 1 ? hs.q_stack : 0;
-    // Stage nodes + triangles + 4-wide nodes in LDS when they fit in 64 KB (the
-    // Cornell presets need ~6 KB).
     {
-        const size_t sb = hs.nodes.size() * sizeof(DNode) + hs.tris.size() * sizeof(DTri) +
-                          ((hs.mats.size() * sizeof(DMat) + 15) & ~(size_t)15) + hs.qnodes.size() * sizeof(DQNode) +
-                          (hs.leaves.size() + hs.groups.size()) * sizeof(DNode);
-        const char* no = std::getenv("TPT_NO_LDS");
-        ds.lds_bytes = (sb <= 64 * 1024 && !(no && no[0] == '1')) ? (int)sb : 0;
+        ds.lds_bytes = (int)lds_b;
         const char* dbg = std::getenv("TPT_DEBUG_FLAGS");
         ds.dbg = dbg ? std::atoi(dbg) : 0;
         ds.dbgc = c->counters + 8;

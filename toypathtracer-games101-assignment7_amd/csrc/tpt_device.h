@@ -222,7 +222,49 @@ TPT_D Hit traverse_t(const DScene& s, int root, const Ray& r, int cull, int* /*s
 // triangles) this beats a per-lane walk; rays with an infinite inv component keep
 // the walk.
 enum { kFlatShadow = 1, kFlatHit = 2, kFlatPkShadow = 4 };
-constexpr int kFlatMaxLeaves = 64;
+// A walk group (groups[g].b < 0) is a mesh too large for the flat list (the bunny):
+// a lane whose ray passed the group box -- the mesh root's box, tpt_scene.h -- walks
+// the mesh's threaded subtree from the root's right child (a) until kMeshExit, i.e.
+// exactly the reference's DFS below that box, at the group's place in the leaf
+// order.  Nodes and triangles come through L2 (s.tnodes / s.tris).
+TPT_D void walk_group_closest(const DScene& s, int cur, const Ray& r, int cull, Hit& best) {
+    while (cur >= 0) {
+        const DNode n = s.tnodes[cur];
+        int nxt = n.b;
+        if (box_hit_t<true>(n, r)) {
+            if (n.a >= 0) {
+                nxt = n.a;
+            } else if (n.a != kEmptyLeaf) {
+                const int prim = -1 - n.a;
+                double dist;
+                if (tri_test(s.tris[prim], r, cull, dist) && (best.prim < 0 || best.dist > dist)) {
+                    best.dist = dist;
+                    best.prim = prim;
+                }
+            }
+        }
+        cur = nxt;
+    }
+}
+TPT_D bool walk_group_shadow(const DScene& s, int cur, const Ray& r, V3 lc, double thr, int cull) {
+    while (cur >= 0) {
+        const DNode n = s.tnodes[cur];
+        int nxt = n.b;
+        if (box_hit_t<true>(n, r)) {
+            if (n.a >= 0) {
+                nxt = n.a;
+            } else if (n.a != kEmptyLeaf) {
+                double dist;
+                if (tri_test(s.tris[-1 - n.a], r, cull, dist)) {
+                    const V3 hx = r.o + mul(r.d, (float)dist);
+                    if (dot3(hx - lc, hx - lc) < thr) return true;
+                }
+            }
+        }
+        cur = nxt;
+    }
+    return false;
+}
 // Objects are tested first (their box is the union of their leaves' boxes, so a
 // failed object box means every leaf box of it fails): a wave skips the leaves of an
 // object no lane's ray reaches.
@@ -232,8 +274,12 @@ TPT_D Hit traverse_flat(const DScene& s, const Ray& r, int cull) {
     best.dist = 0.0;
     for (int gi = 0; gi < s.ngroup; ++gi) {
         const DNode gn = s.groups[gi];
-        if (__ballot(slab_hit_finite(gn.bmin[0], gn.bmin[1], gn.bmin[2], gn.bmax[0], gn.bmax[1], gn.bmax[2], r)) == 0)
+        const bool pass = slab_hit_finite(gn.bmin[0], gn.bmin[1], gn.bmin[2], gn.bmax[0], gn.bmax[1], gn.bmax[2], r);
+        if (__ballot(pass) == 0) continue;
+        if (gn.b < 0) {
+            if (pass) walk_group_closest(s, gn.a, r, cull, best);
             continue;
+        }
         const int j1 = gn.a + gn.b;
         for (int j = gn.a; j < j1; ++j) {
             const DNode n = s.leaves[j];
@@ -241,7 +287,7 @@ TPT_D Hit traverse_flat(const DScene& s, const Ray& r, int cull) {
                 const int prim = -1 - n.a;
                 double dist;
                 bool h;
-                if (prim < s.ntri) h = tri_test(s.tris[prim], r, cull, dist);
+                if (prim < s.ntri) h = tri_test(s.ftris[n.b], r, cull, dist);
                 else h = sphere_test(s.sph[prim - s.ntri], r, cull, dist);
                 if (h && (best.prim < 0 || best.dist > dist)) {
                     best.dist = dist;
@@ -257,9 +303,13 @@ TPT_D bool shadow_flat(const DScene& s, const Ray& r, V3 lc, double thr, int cul
     bool sh = false;
     for (int gi = 0; gi < s.ngroup; ++gi) {
         const DNode gn = s.groups[gi];
-        if (__ballot(!sh && slab_hit_finite(gn.bmin[0], gn.bmin[1], gn.bmin[2], gn.bmax[0], gn.bmax[1], gn.bmax[2],
-                                            r)) == 0)
+        const bool pass =
+            !sh && slab_hit_finite(gn.bmin[0], gn.bmin[1], gn.bmin[2], gn.bmax[0], gn.bmax[1], gn.bmax[2], r);
+        if (__ballot(pass) == 0) continue;
+        if (gn.b < 0) {
+            if (pass) sh = walk_group_shadow(s, gn.a, r, lc, thr, cull);
             continue;
+        }
         const int j1 = gn.a + gn.b;
         for (int j = gn.a; j < j1; ++j) {
             const DNode n = s.leaves[j];
@@ -267,7 +317,7 @@ TPT_D bool shadow_flat(const DScene& s, const Ray& r, V3 lc, double thr, int cul
                 const int prim = -1 - n.a;
                 double dist;
                 bool h;
-                if (prim < s.ntri) h = tri_test(s.tris[prim], r, cull, dist);
+                if (prim < s.ntri) h = tri_test(s.ftris[n.b], r, cull, dist);
                 else h = sphere_test(s.sph[prim - s.ntri], r, cull, dist);
                 if (h) {
                     const V3 hx = r.o + mul(r.d, (float)dist);
@@ -1349,6 +1399,82 @@ TPT_D V3 pt_sample(const DScene& s, PixPark px, uint32_t& rs, int* stk, Packet p
         result = result + ev * load_mat(s, o.mat).em;
     }
     return result;
+}
+
+// ------------------------------------------------ PT, indirect bounce on ---
+// TPT_MODE_PT_INDIRECT: PathTracer.cpp:44-134 with the `break` at :109 removed.
+// One iteration of the loop body after its closest hit `v` (:64-131): emission on
+// the first hit only (lastBounceExplicitSampledLight is false only until the first
+// light loop, :50/:80), MIS direct lighting from every emitter weighted by the
+// throughput alpha, then the BSDF-sampled continuation with Russian roulette after
+// five bounces (the coin is drawn only then, :122-123).  Updates the ray, alpha,
+// radiance, bounce count and culling flip in place; false when the path ends.
+struct PtiPath {
+    Ray r;
+    V3 alpha, res;
+    int nb;     // outBounces
+    bool flip;  // lastBounceFlipCulling
+};
+TPT_D bool pti_step(const DScene& s, const PTV& v, PtiPath& p, uint32_t& rs, int* stk, Packet pk) {
+    const int mi = prim_mat(s, v.prim);
+    const Mat m = load_mat(s, mi);
+    if (p.nb == 0 && s.mats[mi].has_em) p.res = p.res + p.alpha * m.em;  // :64-68
+    const V3 x = v.x, wo = -p.r.d;
+    const Shade sh = make_shade(v.N, wo);
+    float pdf_b;
+    const V3 wib = mat_sample(m, wo, sh, &pdf_b, rs);  // :76
+    for (int li = 0; li < s.n_emitters; ++li) {        // :82-106, as pt_sample
+        const DObj o = s.objs[s.emitters[li]];
+        V3 pc, pn;
+        int pp;
+        object_sample(s, o, pc, pn, pp, rs);
+        V3 wil = pc - x;
+        const float d2 = (float)dot3(wil, wil);
+        wil = normalized(wil);
+        const float ct = (float)dot3(pn, -wil);
+        const float pll = (float)((double)o.pdf * d2 / (double)fabs_(ct));
+        V3 ev = v3s(0.0f);
+        {
+            const Ray rb = make_ray(x, wib);
+            Hit hnc, hb;
+            object_hit_nocull_back(s, o, rb, hnc, hb, stk);
+            float pbl = 0.0f;
+            if (hnc.prim >= 0) {
+                V3 hx, hn;
+                hit_geometry(s, rb, hnc, hx, hn);
+                const float ld2 = (float)dot3(hx - x, hx - x);
+                const float c = (float)dot3(hn, -wib);
+                if (c != 0.0f) pbl = (float)((double)o.pdf * ld2 / (double)fabs_(c));
+            }
+            if (pdf_b + pbl > 0.0f && hb.prim >= 0) {
+                V3 hx, hn;
+                hit_geometry(s, rb, hb, hx, hn);
+                if (!shadow_q_packet(s, hx, x, TPT_CULL_BACK, pk))
+                    ev = ev + divs(eval_bsdf(m, wo, wib, sh, true), 1e-4f + pdf_b + pbl);
+            }
+        }
+        const float plb = mat_pdf(m, wo, sh, wil);
+        if (pll + plb > 0.0f) {
+            const Ray rl = make_ray(x, wil);
+            const Hit hl = object_hit(s, o, rl, TPT_CULL_BACK, stk);
+            V3 hx = v3s(0.0f), hn;  // default Intersection::coords when missed
+            if (hl.prim >= 0) hit_geometry(s, rl, hl, hx, hn);
+            if (!shadow_q_packet(s, hx, x, TPT_CULL_BACK, pk))
+                ev = ev + divs(eval_bsdf(m, wo, wil, sh, true), 1e-4f + pll + plb);
+        }
+        p.res = p.res + p.alpha * ev * load_mat(s, o.mat).em;  // :105
+    }
+    V3 weight = v3s(0.0f);  // :111-114
+    if (pdf_b > 0.0f) weight = divs(eval_bsdf(m, wo, wib, sh, true), 1e-4f + pdf_b);
+    p.r = make_ray(x, wib);             // :116
+    p.flip = dot3(v.N, wib) < 0.0;      // :117-120
+    const bool rr = p.nb > 4;           // :122
+    if (!rr || rng_float(rs) < 0.8f) {  // :123-127
+        p.alpha = divs(p.alpha * weight, rr ? 0.8f : 1.0f);
+        p.nb += 1;
+        return true;
+    }
+    return false;
 }
 
 // Camera (SceneRenderingHelper.cpp:16-22); scale is host-computed CalculateScale.

@@ -40,6 +40,11 @@ static const int32_t kSpliceBit = 0x40000000;
 static const int32_t kWalkEnd = -1;
 static const int32_t kMeshExit = -2;
 
+// Flat queries (tpt_device.h) list at most this many primitive leaves.  A scene
+// with more keeps its largest meshes out of the list as walk groups
+// (tpt_scene_build.cpp: split_walk_groups).
+static const int kFlatMaxLeaves = 64;
+
 // 128 B: a 4-wide node for shadow (any-hit) queries, made by collapsing two levels
 // of the binary tree (tpt_scene_build.cpp: build_qnodes).  Child j's box is the
 // binary node's own box; child >= 0 is another DQNode, child < 0 a leaf as in
@@ -110,7 +115,9 @@ struct DScene {
     const DQNode* qnodes;     // 4-wide shadow tree, root at 0
     const DNode* tnodes;      // threaded binary tree (stackless walks), same indices as nodes
     const DNode* leaves;      // primitive leaves in the reference's DFS order (flat queries)
-    const DNode* groups;      // leaves grouped per object: box, a = first leaf, b = count
+    const DNode* groups;      // leaves grouped per object: box, a = first leaf, b = count;
+                              // b < 0: walk group, a = first node of the mesh walk in tnodes
+    const DTri* ftris;        // triangle of flat leaf j is ftris[leaves[j].b]
     int32_t nleaf;
     int32_t ngroup;
     int32_t flat;             // flat (all-leaves) queries: kFlatShadow | kFlatHit | kFlatPkShadow bits, 0 = tree walks
@@ -129,7 +136,8 @@ struct DScene {
     int32_t nmats;
     int32_t max_stack;  // LDS stack entries per lane a binary-tree walk can need (depth + 1)
     int32_t q_stack;    // ... and a per-lane walk of the 4-wide shadow tree (3 per level + 1)
-    int32_t lds_bytes;  // bytes of nodes + triangles + qnodes staged in LDS per workgroup (0 = read from HBM/L2)
+    int32_t lds_bytes;  // bytes staged in LDS per workgroup (0 = read from HBM/L2)
+    int32_t lds_full;   // 1: nodes + triangles + qnodes + flat arrays staged; 0: only the flat arrays
     int32_t dbg;        // ablation switches for profiling only (TPT_DEBUG_FLAGS); 0 in production
     unsigned long long* dbgc;  // profiling counters (TPT_DEBUG_FLAGS & 2)
 };

@@ -186,6 +186,40 @@ static void thread_tree(HostScene& hs, int n, int after, int ntop, bool scene) {
     thread_tree(hs, src.a, after, ntop, scene);
 }
 
+// Flat queries test every listed leaf; past kFlatMaxLeaves the largest meshes leave
+// the list and become walk groups {box, a = gwalk, b = -1}: a lane whose ray passes
+// the group box (the mesh root's box) walks the mesh subtree on the threaded tree,
+// at the group's place in the DFS order, so the visit order is still the reference's.
+static void split_walk_groups(HostScene& hs, const std::vector<int>& gwalk) {
+    int total = (int)hs.leaves.size();
+    if (total <= kFlatMaxLeaves) return;
+    std::vector<int> order(hs.groups.size());
+    for (size_t g = 0; g < order.size(); ++g) order[g] = (int)g;
+    std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return hs.groups[x].b > hs.groups[y].b; });
+    std::vector<char> walk(hs.groups.size(), 0);
+    for (int g : order) {
+        if (total <= kFlatMaxLeaves) break;
+        if (gwalk[g] < 0) continue;
+        walk[g] = 1;
+        total -= hs.groups[g].b;
+    }
+    std::vector<DNode> leaves, groups;
+    for (size_t g = 0; g < hs.groups.size(); ++g) {
+        DNode G = hs.groups[g];
+        if (walk[g]) {
+            G.a = gwalk[g];
+            G.b = -1;
+        } else {
+            const int a0 = G.a;
+            G.a = (int)leaves.size();
+            leaves.insert(leaves.end(), hs.leaves.begin() + a0, hs.leaves.begin() + a0 + G.b);
+        }
+        groups.push_back(G);
+    }
+    hs.leaves.swap(leaves);
+    hs.groups.swap(groups);
+}
+
 static void build_threads(HostScene& hs, int ntop, const std::vector<int>& mesh_root) {
     hs.tnodes.assign(hs.nodes.size(), DNode{});
     hs.leaves.clear();
@@ -200,6 +234,7 @@ static void build_threads(HostScene& hs, int ntop, const std::vector<int>& mesh_
     // its group box is the scene-level leaf box (= the mesh root box); a sphere is a
     // group of one.  groups[g] = {box, a = first leaf, b = leaf count}.
     hs.groups.clear();
+    std::vector<int> gwalk;  // per group: first node of its mesh walk (the root's right child), -1 if none
     int cur = 0, cont = kWalkEnd;
     while (cur >= 0) {
         const DNode& n = hs.tnodes[cur];
@@ -212,6 +247,7 @@ static void build_threads(HostScene& hs, int ntop, const std::vector<int>& mesh_
                 g.a = (int)hs.leaves.size();
                 g.b = 0;
                 hs.groups.push_back(g);
+                gwalk.push_back(nxt);
             } else {
                 nxt = n.a;
             }
@@ -223,6 +259,7 @@ static void build_threads(HostScene& hs, int ntop, const std::vector<int>& mesh_
                 g.a = (int)hs.leaves.size();
                 g.b = 0;
                 hs.groups.push_back(g);
+                gwalk.push_back(-1);
             }
             hs.leaves.push_back(l);
             hs.groups.back().b++;
@@ -234,6 +271,7 @@ static void build_threads(HostScene& hs, int ntop, const std::vector<int>& mesh_
             cur = nxt;
         }
     }
+    split_walk_groups(hs, gwalk);
 }
 
 int build_host_scene(const tpt_scene_desc* d, HostScene& hs, std::string& err) {

@@ -149,7 +149,7 @@ void Renderer::Render(std::string out, const Scene& scene, int spp, int thread_c
         tpt_render_params p;
         std::memset(&p, 0, sizeof(p));
         p.spp = spp;
-        p.mode = bdpt ? TPT_MODE_BDPT : TPT_MODE_PT;
+        p.mode = bdpt ? TPT_MODE_BDPT : opt.pt_indirect ? TPT_MODE_PT_INDIRECT : TPT_MODE_PT;
         p.pixel_begin = 0;
         p.pixel_stride = 1;
         rc = tpt_render(ctx, &p, framebuffer.data(), bdpt ? splat.data() : nullptr, &stats);

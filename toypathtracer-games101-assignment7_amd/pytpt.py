@@ -21,6 +21,7 @@ TPT_E_NOSCENE = -3
 TPT_E_ALLOC = -4
 TPT_E_UNSUPPORTED = -5
 MODE_PT, MODE_BDPT = 0, 1
+MODE_PT_INDIRECT = 2  # PathTrace without the HEAD `break` (PathTracer.cpp:109); off by default
 CULL_BACK, CULL_FRONT, NO_CULL = 0, 1, 2
 PRESETS = ("silver", "standard", "refractive_ball", "occlusion", "smooth_dielectric", "bunny")
 
