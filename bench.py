@@ -34,7 +34,10 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 # SURVEY.md §8(d) / BASELINE.md: algorithmic bytes per sample (reference traversal counts)
 B_ALG = {("standard", "pt"): 2073, ("standard", "bdpt"): 18481, ("refractive_ball", "pt"): 2109,
-         ("refractive_ball", "bdpt"): 19377, ("bunny", "pt"): 2123, ("bunny", "bdpt"): 21229}
+         ("refractive_ball", "bdpt"): 19377, ("bunny", "pt"): 2123, ("bunny", "bdpt"): 21229,
+         # scripts/b_alg.py (oracle traversal counts, full frame at 1 spp; reproduces the six above)
+         ("smooth_dielectric", "pt"): 2076, ("smooth_dielectric", "bdpt"): 26715,
+         ("silver", "pt"): 2075, ("silver", "bdpt"): 25386}
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
 
 

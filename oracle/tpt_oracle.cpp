@@ -49,6 +49,10 @@ namespace orc {
 // global.cpp:5-13 (shifts 13, 17, 15), :15-17, :19-22.  thread_local state as
 // Random.cpp:5.
 static thread_local uint32_t rnd_state = 1;
+// Traversal counters behind SURVEY.md §8(d)'s algorithmic bytes: BVH nodes popped
+// (top + mesh BVHs, BVH.cpp:113) and triangle tests (Triangle.cpp:77).  Read by
+// oracle_traversal_counts only.
+static thread_local uint64_t cnt_nodes = 0, cnt_tris = 0;
 static inline uint32_t xorshift32() {
     uint32_t x = rnd_state;
     x ^= x << 13;
@@ -585,8 +589,10 @@ struct Scene {
         stack[sp++] = 0;
         while (sp) {
             const Node& n = nodes[stack[--sp]];
+            ++cnt_nodes;
             if (!box_hit(n.b, ray)) continue;
             if (n.item >= 0) {
+                ++cnt_tris;
                 Hit t = tri_hit(n.item, ray, cull);
                 if (t.happened && (!best.happened || best.distance > t.distance)) best = t;
             } else if (sp + 2 < 64) {
@@ -608,6 +614,7 @@ struct Scene {
         stack[sp++] = 0;
         while (sp) {
             const Node& n = top[stack[--sp]];
+            ++cnt_nodes;
             if (!box_hit(n.b, ray)) continue;
             if (n.item >= 0) {
                 Hit t = object_hit(n.item, ray, cull);
@@ -1284,6 +1291,18 @@ double oracle_render(void* h, int mode, int spp, int threads, int64_t pixel_limi
             }
     auto t1 = std::chrono::steady_clock::now();
     return std::chrono::duration<double, std::milli>(t1 - t0).count();
+}
+
+// SURVEY.md §8(d) B_alg: node pops and triangle tests of the reference traversal
+// over the given pixels at `spp` (the oracle is single-threaded here).  out[0] =
+// nodes, out[1] = triangle tests, both totals.
+void oracle_traversal_counts(void* h, int mode, int spp, const int64_t* pix, int64_t n, uint64_t* out) {
+    std::vector<float> rgb(3 * (size_t)n), splat;
+    Scene* s = (Scene*)h;
+    if (mode == TPT_MODE_BDPT) splat.resize(3 * (size_t)s->width * s->height);
+    cnt_nodes = cnt_tris = 0;
+    oracle_trace_pixels(h, mode, spp, pix, n, rgb.data(), splat.empty() ? nullptr : splat.data(), nullptr);
+    out[0] = cnt_nodes; out[1] = cnt_tris;
 }
 
 void oracle_rng(uint32_t seed, int n, uint32_t* u, float* f) {

@@ -36,6 +36,7 @@ class Oracle:
         L.oracle_render.argtypes = [P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int64, P]
         L.oracle_render.restype = ctypes.c_double
         L.oracle_rng.argtypes = [ctypes.c_uint32, ctypes.c_int, P, P]
+        L.oracle_traversal_counts.argtypes = [P, ctypes.c_int, ctypes.c_int, P, ctypes.c_int64, P]
         L.oracle_intersect.argtypes = [P, P, ctypes.c_int64, ctypes.c_int, P]
         L.oracle_material_kat.argtypes = [P, P, ctypes.c_int, P]
         L.oracle_helper_kat.argtypes = [P, ctypes.c_int, P]
@@ -58,6 +59,13 @@ class Oracle:
         b = np.zeros(len(pix), np.int64)
         self.L.oracle_trace_pixels(P(self.h), mode, spp, _p(pix), len(pix), _p(out), _p(splat), _p(b))
         return out, (splat.reshape(self.height, self.width, 3) if want_splat else None), b
+
+    def traversal_counts(self, mode, spp, pix):
+        """(nodes popped, triangle tests) summed over `pix` x `spp` (SURVEY §8(d) B_alg)."""
+        pix = np.ascontiguousarray(pix, np.int64)
+        out = np.zeros(2, np.uint64)
+        self.L.oracle_traversal_counts(P(self.h), mode, spp, _p(pix), len(pix), _p(out))
+        return int(out[0]), int(out[1])
 
     def render(self, mode, spp, threads=1, pixel_limit=0):
         out = np.zeros(self.width * self.height * 3, np.float32)

@@ -119,3 +119,15 @@ def test_live_indirect_against_reference(preset):
     R, o = Reference(preset), Oracle(preset)
     a, b = o.trace_pixels(2, 8, pix), R.trace_pixels(2, 8, pix)
     assert eq_bits(a[0], b[0]) and np.array_equal(a[2], b[2])
+
+
+def test_traversal_counts_b_alg():
+    """bench.py's B_ALG (nodes x 32 B + triangle tests x 48 B per sample)
+    against the oracle's traversal counters on every 7th pixel of the Standard frame."""
+    import bench
+    o = Oracle("standard")
+    pix = np.arange(0, 784 * 784, 7, dtype=np.int64)
+    for mode, name in ((0, "pt"), (1, "bdpt")):
+        nodes, tris = o.traversal_counts(mode, 1, pix)
+        b = (nodes * 32 + tris * 48) / len(pix)
+        assert abs(b / bench.B_ALG[("standard", name)] - 1) < 0.01, (name, b)
