@@ -1,24 +1,35 @@
 """bench.py -- Msamples/s (pixels x spp / s) of the integration loop on MI355X.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--mode pt|bdpt] [--scene S] [--spp SPP]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--mode pt|bdpt|c5|pti] [--scene S] [--spp SPP]
 
-A step is one full render of the 784x784 frame (BASELINE.json configs[1]:
-Standard Cornell Box, PT, 1024 spp on 1 MI355X).  With N > 1 (launched by
-torch.distributed.run) each rank renders its pixel shard (i = rank; i += N, the
-reference's own interleave, Renderer.cpp:38) into HBM and the framebuffers are
-summed onto rank 0 with one RCCL reduce over xGMI; per-GPU work is
-fixed by the frame, so scaling is strong.  Inputs (the flattened scene) are
-resident in HBM before timing; the timed region is render + reduce.
+With no --mode the ONE JSON line carries three workloads, each a full 784x784 frame
+per step with the flattened scene already resident in HBM:
+  * the headline, BASELINE.json configs[1]: Standard Cornell Box, PT, 1024 spp;
+  * "bdpt": configs[2], Standard Cornell Box, BDPT, 256 spp;
+  * "c5":   configs[4], Cornell + bunny, BDPT, 4096 spp (one frame: ~19 s on one GPU).
+--mode runs one workload alone (profiling runs use it).
 
-Roofline: the hot kernel's ALGORITHMIC scene-fetch bytes (BVH nodes
-popped x 32 B + triangle tests x 48 B, counted on the reference traversal; 2,073 B
-per Standard PT sample) / its average device time (HIP events inside libtpt on the
-stream the kernel runs on) against 8 TB/s.  The scene is L2-resident, so this is a
-modelled yardstick; `traffic` is the memory-side bytes per launch measured by
-rocprofv3 FETCH_SIZE/WRITE_SIZE passes (profiles/traffic.json, scripts/pmc_traffic.py).
+With N > 1 (launched by torch.distributed.run, one process per GPU) each rank
+renders its pixel shard (i = rank; i += N, the reference's own interleave,
+Renderer.cpp:38) into HBM and the [rgb; splat] buffer is summed onto rank 0 with one
+RCCL reduce over xGMI.  The frame is fixed as N grows: strong scaling.
+The timed region is render + reduce, bracketed by barrier + synchronize, max over ranks.
+
+roofline: the dominant kernel's VALU issue rate.  Nothing on this path is a dense
+contraction and the scene is LDS/L2-resident, so the bound is vector-instruction
+issue.  profiles/valu_model.json (scripts/valu_model.py) holds the
+kernel's SIMD issue-cycles per launch = sum over instruction classes of
+rocprofv3 SQ_INSTS_VALU_* counts x the cycles per wave-instruction measured on
+MI355X by scripts/valu_cost.hip; `achieved` divides that by the kernel's average
+duration measured live here (HIP events inside libtpt on the stream the kernel runs
+on); `peak` = 1,024 SIMDs x the clock the profiled run held (GRBM_GUI_ACTIVE).
+roofline_hbm_model: SURVEY §8(d)'s modelled HBM yardstick (algorithmic scene-fetch
+bytes / kernel time / 8 TB/s); `traffic` is the measured memory-side bytes per launch
+(profiles/traffic.json).
 
 cpu_baseline: the REAL reference renderer (oracle/_ref/libref.so, Renderer::Render
-with std::async threads) on a bounded sample, rank 0 only; falls back to the CPU
+with std::async threads, one per CPU this process may run on) on a bounded sample,
+rank 0 at N = 1 only, plus the -j 1 leg of configs[0]; falls back to the CPU
 restatement (oracle/liboracle.so, kind "port") if the reference build is absent.
 """
 import argparse
@@ -39,158 +50,278 @@ B_ALG = {("standard", "pt"): 2073, ("standard", "bdpt"): 18481, ("refractive_bal
          ("smooth_dielectric", "pt"): 2076, ("smooth_dielectric", "bdpt"): 26715,
          ("silver", "pt"): 2075, ("silver", "bdpt"): 25386}
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
+N_SIMD = 1024          # 256 CUs x 4 SIMDs
+MAX_CLOCK_MHZ = 2400.0
+
+# (scene, mode, spp) of each workload; BASELINE.json configs[1], [2], [4]
+WORKLOADS = {"pt": ("standard", "pt", 1024), "bdpt": ("standard", "bdpt", 256), "c5": ("bunny", "bdpt", 4096),
+             "pti": ("standard", "pti", 1024)}
+CONFIG_NAME = {"pt": "configs[1]: Standard Cornell Box 784x784, PT, 1024 spp",
+               "bdpt": "configs[2]: Standard Cornell Box 784x784, BDPT, 256 spp",
+               "c5": "configs[4]: Cornell + bunny OBJ 784x784, BDPT, 4096 spp, pixel-sharded + RCCL reduce",
+               "pti": "PathTrace with the indirect bounce (not a BASELINE config), Standard 784x784, 1024 spp"}
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=5, help="timed frames of the headline PT workload")
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--mode", choices=("pt", "bdpt", "pti"), default="pt",
-                    help="pti: PathTrace with the indirect bounce on (TPT_MODE_PT_INDIRECT, not a BASELINE config)")
-    ap.add_argument("--scene", default="standard")
-    ap.add_argument("--spp", type=int, default=None, help="default 1024 (PT) / 256 (BDPT), BASELINE configs 1-2")
-    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--mode", choices=("pt", "bdpt", "c5", "pti"), default=None,
+                    help="run one workload alone (default: PT headline + bdpt + c5 in one line)")
+    ap.add_argument("--scene", default=None, help="override the workload's scene")
+    ap.add_argument("--spp", type=int, default=None, help="override the workload's spp")
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline legs")
+    ap.add_argument("--no-c5", action="store_true", help="default line without the c5 sub-object")
     ap.add_argument("--cpu-threads", type=int, default=None)
-    ap.add_argument("--traffic-bytes", type=float, default=None,
-                    help="HBM bytes per launch (default: profiles/traffic.json, made by scripts/pmc_traffic.py)")
     return ap.parse_args()
 
 
-def pmc_traffic(scene, mode):
-    """Per-launch memory-side bytes of the dominant kernel, measured by rocprofv3
-    FETCH_SIZE / WRITE_SIZE passes of this build (profiles/traffic.json)."""
-    path = os.path.join(ROOT, "profiles", "traffic.json")
-    if not os.path.exists(path):
-        return None
-    e = json.load(open(path)).get("%s/%s" % (scene, mode))
-    return float(e["bytes_per_launch"]) if e else None
+def _load_json(name):
+    path = os.path.join(ROOT, "profiles", name)
+    return json.load(open(path)) if os.path.exists(path) else {}
 
 
-def cpu_baseline(mode, scene, threads):
-    """Bounded CPU sample on this host (about 10-30 s of CPU work)."""
-    import numpy as np
+def cpu_info():
+    """Host CPU as this process sees it: model, nproc, the CPUs it may run on and the
+    cgroup CPU quota (the GPU box shares its host between jobs)."""
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    affinity = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = float(q) / float(period)
+    except (OSError, ValueError):
+        pass
+    return {"model": model, "nproc": os.cpu_count(), "affinity": affinity, "cgroup_cpus": quota}
+
+
+def _quiet(fn):
+    """Run fn() with fd 1 redirected: the reference prints progress from C++."""
+    import ctypes
+    sys.stdout.flush()
+    saved = os.dup(1)
+    devnull = os.open(os.devnull, os.O_WRONLY)
+    os.dup2(devnull, 1)
+    try:
+        return fn()
+    finally:
+        ctypes.CDLL(None).fflush(None)
+        os.dup2(saved, 1)
+        os.close(saved)
+        os.close(devnull)
+
+
+def cpu_render(scene, mode, spp, threads):
+    """Wall seconds of one full-frame render on the CPU; (seconds, kind)."""
     from oracle_bind import Oracle, Reference, ref_available
-    spp = {"pt": 64, "pti": 16}.get(mode, 2)
     m = {"pt": 0, "bdpt": 1, "pti": 2}[mode]
     # Renderer::Render has no switch for the indirect bounce: for "pti" the baseline is
     # the restatement (bit-exact to the reference built without PathTracer.cpp:109)
     if ref_available() and mode != "pti":
-        # the reference prints its progress lines from C++ (fd 1): keep them off the
-        # bench's one-JSON-line stdout
-        sys.stdout.flush()
-        saved = os.dup(1)
-        devnull = os.open(os.devnull, os.O_WRONLY)
-        os.dup2(devnull, 1)
-        try:
-            R = Reference(scene)
+        R = Reference(scene)
+
+        def run():
             t0 = time.perf_counter()
             R.render(m, spp, threads=threads)
-            dt = time.perf_counter() - t0
-        finally:
-            import ctypes
-            ctypes.CDLL(None).fflush(None)  # C stdio buffers still hold reference output
-            os.dup2(saved, 1)
-            os.close(saved)
-            os.close(devnull)
-        kind = "reference"
-    else:
-        o = Oracle(scene)
-        _, ms = o.render(m, spp, threads=threads)
-        dt = ms / 1e3
-        kind = "port"
+            return time.perf_counter() - t0
+        return _quiet(run), "reference"
+    _, ms = Oracle(scene).render(m, spp, threads=threads)
+    return ms / 1e3, "port"
+
+
+def cpu_baseline(key, scene, mode, threads, info):
+    """Bounded CPU sample of the workload on this host: full frames at a reduced spp
+    (throughput does not depend on spp: the per-pixel stream is serial either way)."""
+    spp = {"pt": 64, "pti": 16, "bdpt": 2}[mode] if key != "c5" else 1
+    dt, kind = cpu_render(scene, mode, spp, threads)
+    if dt < 2.0 and mode == "pt":  # many-core host: lengthen the sample to a few seconds
+        spp *= max(2, int(round(4.0 / max(dt, 1e-3))))
+        dt, kind = cpu_render(scene, mode, spp, threads)
     n = 784 * 784 * spp
-    return {"value": round(n / dt / 1e6, 4), "unit": "Msamples/s", "cores": threads, "kind": kind,
-            "sample": "full 784x784 %s frame of '%s' at %d spp, Renderer::Render with %d std::async threads, "
-                      "wall %.2f s" % (mode.upper(), scene, spp, threads, dt)}
+    cores = threads if info["cgroup_cpus"] is None else min(threads, info["cgroup_cpus"])
+    out = {"value": round(n / dt / 1e6, 4), "unit": "Msamples/s", "cores": cores, "threads": threads,
+           "kind": kind,
+           "sample": "full 784x784 %s frame of '%s' at %d spp, Renderer::Render with %d std::async threads, "
+                     "wall %.2f s" % (mode.upper(), scene, spp, threads, dt),
+           "host": info}
+    if key == "pt":
+        # BASELINE.json configs[0]: Standard PT 16 spp with -j 1, sampled at 4 spp
+        dt1, kind1 = cpu_render(scene, mode, 4, 1)
+        out["j1"] = {"value": round(784 * 784 * 4 / dt1 / 1e6, 4), "unit": "Msamples/s", "cores": 1,
+                     "kind": kind1, "sample": "configs[0] (-j 1) at 4 spp instead of 16: full 784x784 PT frame "
+                                              "of 'standard', Renderer::Render with 1 thread, wall %.2f s" % dt1}
+    return out
+
+
+def valu_roofline(key, kernel_ms, shard_frac):
+    """VALU-issue roofline of the workload's dominant kernel (see module docstring)."""
+    model = _load_json("valu_model.json").get(key)
+    if not model:
+        return {"bound": "valu", "achieved": None, "peak": None, "unit": "G SIMD-cycles/s", "frac": None,
+                "traffic": None, "note": "profiles/valu_model.json has no entry for %s" % key}
+    cyc = model["issue_cycles_per_launch"] * shard_frac  # this rank's share of the frame
+    ms = kernel_ms
+    achieved = cyc / (ms / 1e3) / 1e9
+    clk = model.get("clock_mhz") or MAX_CLOCK_MHZ
+    peak = N_SIMD * clk / 1e3
+    return {"bound": "valu", "achieved": round(achieved, 1), "peak": round(peak, 1), "unit": "G SIMD-cycles/s",
+            "frac": round(achieved / peak, 4), "frac_at_2400mhz": round(achieved / (N_SIMD * MAX_CLOCK_MHZ / 1e3), 4),
+            "traffic": model.get("hbm_bytes_per_launch"), "kernel": model["kernel"], "kernel_ms": round(ms, 3),
+            "issue_cycles_per_launch": round(cyc), "clock_mhz": clk,
+            "source": model.get("source"),
+            "note": "VALU issue cycles per launch (PMC class counts x measured cycles per wave-instruction, "
+                    "profiles/valu_model.json) / live kernel time / (1,024 SIMDs x the profiled clock)"}
+
+
+def hbm_model(scene, mode, kernel_ms, samples, traffic_key):
+    b_alg = B_ALG.get((scene, "pt" if mode == "pti" else mode))
+    if not b_alg:
+        return None
+    achieved = samples * b_alg / (kernel_ms / 1e3) / 1e9
+    t = _load_json("traffic.json").get(traffic_key)
+    return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": float(t["bytes_per_launch"]) if t else None,
+            "bytes_per_sample_alg": b_alg, "samples_per_launch": samples,
+            "note": "MODEL (SURVEY 8d): algorithmic scene-fetch bytes / kernel time; the scene is LDS/L2-resident, "
+                    "so frac > 1 is cache reuse, not a violated bound; traffic = measured memory-side bytes per launch"}
+
+
+class Runner:
+    def __init__(self, args):
+        import torch
+        self.torch = torch
+        self.args = args
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        if args.gpus > 1 and self.world == 1:
+            sys.exit("--gpus > 1 must be launched with torch.distributed.run (one process per GPU)")
+        self.dist = None
+        if self.world > 1:
+            import torch.distributed as dist
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            self.dist = dist
+        else:
+            torch.cuda.set_device(0)
+        import pytpt
+        import sharding
+        self.pytpt, self.sharding = pytpt, sharding
+        self.ctx = pytpt.Context(torch.cuda.current_device())
+        self.scene = None
+        self.fb = None
+
+    def barrier(self):
+        self.torch.cuda.synchronize()
+        if self.dist is not None:
+            self.dist.barrier()
+        self.torch.cuda.synchronize()
+
+    def run(self, key, steps, warmup):
+        torch, pytpt = self.torch, self.pytpt
+        scene, mode, spp = WORKLOADS[key]
+        if self.args.mode is not None:
+            scene = self.args.scene or scene
+            spp = self.args.spp or spp
+        if self.scene != scene:
+            self.ctx.upload(pytpt.Preset(scene))
+            self.scene = scene
+        W, H = self.ctx.width, self.ctx.height
+        if self.fb is None or self.fb.shape[1] != H * W * 3:
+            self.fb = torch.zeros(2, H * W * 3, dtype=torch.float32, device="cuda")  # rgb + splat, one reduce
+        fb = self.fb
+        m = {"pt": pytpt.MODE_PT, "bdpt": pytpt.MODE_BDPT, "pti": pytpt.MODE_PT_INDIRECT}[mode]
+        begin, stride = self.sharding.shard(self.rank, self.world)  # Renderer.cpp:38 interleave
+        stream = torch.cuda.current_stream()
+
+        def step():
+            # libtpt renders on its own stream: everything torch's stream has queued on
+            # fb (the zero fill, the previous step's reduce) must finish before it
+            # rewrites the buffers.
+            stream.synchronize()
+            st = self.ctx.render_device(spp, m, fb[0].data_ptr(), fb[1].data_ptr(), begin, stride)
+            self.sharding.reduce_frame(self.dist, fb, dst=0)  # rgb + splat onto rank 0 (RCCL over xGMI)
+            return st
+
+        for _ in range(warmup):
+            step()
+        self.barrier()
+        kms = []
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            st = step()
+            kms.append(st.kernel_ms)
+        self.barrier()
+        dt = time.perf_counter() - t0
+        if self.dist is not None:
+            t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+            self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+            dt = float(t.item())
+        samples = W * H * spp * steps  # all ranks together cover the frame each step
+        kernel_ms = sum(kms) / len(kms)
+        shard_samples = st.samples
+        tkey = "%s/%s" % (scene, mode)
+        line = {"metric": "Msamples/s (pixels x spp / s), %s %s %dx%d" % (scene, mode.upper(), W, H),
+                "value": round(samples / dt / 1e6, 2), "unit": "Msamples/s", "n_gpus": self.world, "steps": steps,
+                "warmup": warmup, "ms_per_step": round(dt / steps * 1e3, 3),
+                "config": {"workload": CONFIG_NAME[key] if self.args.mode is None or
+                           (scene, spp) == WORKLOADS[key][::2] else "%s %s %d spp" % (scene, mode.upper(), spp),
+                           "scene": scene, "mode": mode, "spp": spp, "width": W, "height": H,
+                           "parallelism": "pixel-shard x%d + RCCL reduce" % self.world if self.world > 1
+                           else "1 GPU"},
+                "roofline": valu_roofline(tkey, kernel_ms, shard_samples / float(W * H * spp)),
+                "roofline_hbm_model": hbm_model(scene, mode, kernel_ms, shard_samples, tkey),
+                "kernel_ms_per_step": round(kernel_ms, 3), "samples_per_rank_step": shard_samples}
+        return line
+
+    def close(self):
+        self.ctx.close()
+        if self.dist is not None:
+            self.dist.destroy_process_group()
 
 
 def main():
     a = parse()
-    import numpy as np
-    import torch
-
-    mode = a.mode
-    spp = a.spp or (256 if mode == "bdpt" else 1024)
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if a.gpus > 1 and world == 1:
-        sys.exit("--gpus > 1 must be launched with torch.distributed.run (one process per GPU)")
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(0)
-
-    import pytpt
-    import sharding
-    dev = torch.cuda.current_device()
-    ctx = pytpt.Context(dev)
-    preset = pytpt.Preset(a.scene)
-    ctx.upload(preset)
-    W, H = ctx.width, ctx.height
-    fb = torch.zeros(2, H * W * 3, dtype=torch.float32, device="cuda")  # rgb + splat, one reduce buffer
-    m = {"pt": pytpt.MODE_PT, "bdpt": pytpt.MODE_BDPT, "pti": pytpt.MODE_PT_INDIRECT}[mode]
-    shard_begin, shard_stride = sharding.shard(rank, world)  # Renderer.cpp:38 interleave
-
-    def step():
-        st = ctx.render_device(spp, m, fb[0].data_ptr(), fb[1].data_ptr(), shard_begin, shard_stride)
-        sharding.reduce_frame(dist, fb, dst=0)  # framebuffer + splat sum onto rank 0 (RCCL over xGMI)
-        return st
-
-    for _ in range(a.warmup):
-        step()
-    torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize()
-    kms = []
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        st = step()
-        kms.append(st.kernel_ms)
-    torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
-    if dist is not None:
-        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
-    samples = W * H * spp * a.steps  # all ranks together cover the frame each step
-    value = samples / dt / 1e6
-    if rank == 0:
-        kernel_ms = float(np.mean(kms))
-        shard_samples = st.samples
-        b_alg = B_ALG.get((a.scene, mode))
-        achieved = (shard_samples * b_alg / (kernel_ms / 1e3) / 1e9) if b_alg else None
-        roofline = {"bound": "hbm", "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBS,
-                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
-                    "traffic": a.traffic_bytes if a.traffic_bytes is not None else pmc_traffic(a.scene, mode),
-                    "kernel": {"pt": "tpt_pt_kernel", "pti": "tpt_pti_kernel"}.get(mode, "bdpt wavefront sequence (gen+scan+scatter+conn+fold) x spp"), "kernel_ms": round(kernel_ms, 3),
-                    "bytes_per_sample_alg": b_alg, "samples_per_launch": shard_samples,
-                    "note": "algorithmic scene-fetch bytes (SURVEY 8d); scene is L2-resident, real bound is VALU"}
-        cpu = None
-        if not a.no_cpu and world == 1:
-            threads = a.cpu_threads or min(16, os.cpu_count() or 1)
-            cpu = cpu_baseline(mode, a.scene, threads)
-        line = {"metric": "Msamples/s (pixels x spp / s), %s %s 784x784" % (a.scene, mode.upper()),
-                "value": round(value, 2), "unit": "Msamples/s", "n_gpus": world, "steps": a.steps,
-                "warmup": a.warmup, "ms_per_step": round(dt / a.steps * 1e3, 3), "higher_is_better": True,
-                "scaling": "strong", "vs_baseline": None, "dtype": "f32+f64",
-                "data": "synthetic (deterministic Cornell scene, reference seeds pixel+1)",
-                "config": {"workload": "%s Cornell Box 784x784, %s, %d spp" % (a.scene, mode.upper(), spp),
-                           "scene": a.scene, "mode": mode, "spp": spp, "width": W, "height": H,
-                           "parallelism": "pixel-shard x%d + RCCL reduce" % world if world > 1 else "1 GPU"},
-                "roofline": roofline, "cpu_baseline": cpu}
-        print(json.dumps(line), flush=True)
-    ctx.close()
-    if dist is not None:
-        dist.destroy_process_group()
+    r = Runner(a)
+    info = cpu_info()
+    want_cpu = not a.no_cpu and r.world == 1 and r.rank == 0
+    threads = a.cpu_threads or info["affinity"]
+    keys = [a.mode] if a.mode else ["pt", "bdpt"] + ([] if a.no_c5 else ["c5"])
+    lines = {}
+    for k in keys:
+        if k == keys[0]:
+            steps, warmup = a.steps, a.warmup
+        elif k == "bdpt":
+            steps, warmup = 2, 1      # ~0.63 s per frame on one MI355X
+        else:
+            steps, warmup = 1, 0      # c5: ~19 s per frame on one MI355X
+        lines[k] = r.run(k, steps, warmup)
+    if r.rank == 0:
+        if want_cpu:
+            for k in keys:
+                scene, mode = lines[k]["config"]["scene"], lines[k]["config"]["mode"]
+                lines[k]["cpu_baseline"] = cpu_baseline(k, scene, mode, threads, info)
+        head = lines[keys[0]]
+        out = {"metric": head["metric"], "value": head["value"], "unit": "Msamples/s", "n_gpus": r.world,
+               "steps": head["steps"], "warmup": head["warmup"], "ms_per_step": head["ms_per_step"],
+               "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32+f64",
+               "data": "synthetic (deterministic Cornell scenes, reference seeds pixel+1)",
+               "config": head["config"], "roofline": head["roofline"],
+               "roofline_hbm_model": head["roofline_hbm_model"], "cpu_baseline": head.get("cpu_baseline"),
+               "kernel_ms_per_step": head["kernel_ms_per_step"]}
+        for k in keys[1:]:
+            out[k] = lines[k]
+        print(json.dumps(out), flush=True)
+    r.close()
 
 
 if __name__ == "__main__":

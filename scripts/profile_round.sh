@@ -1,28 +1,45 @@
 #!/usr/bin/env bash
 # On the GPU box: the rocprofv3 evidence behind bench.py's numbers for this build.
-#   scripts/profile_round.sh TAG      -> gpurun_out/prof_TAG/{pt,bdpt}_{kt,fetch,write}/
-# Kernel-trace --stats of the default PT bench and of the BDPT bench (one frame
-# each), then FETCH_SIZE and WRITE_SIZE in separate --pmc passes (MI355X_MICROARCH.md
-# §HBM/rocprofv3: TCC slots do not hold both).  Each step has its own time limit and
-# the script stops at the first failure.
+#   scripts/profile_round.sh TAG [pt|bdpt|c5 ...]   -> gpurun_out/prof_TAG/<workload>_<pass>/
+# Per workload: a kernel-trace --stats pass, then the PMC passes (one rocprofv3 run
+# each, MI355X_MICROARCH.md §rocprofv3 PMC slots: <= 8 SQ, <= 4 TCC of which
+# FETCH_SIZE takes 3 and WRITE_SIZE 2, <= 2 GRBM):
+#   valu1  SQ_INSTS_VALU + the f32 / f64 add, mul, fma and f32 transcendental classes
+#   valu2  f64 transcendental, int32, int64, cvt classes, VALU / wave / busy cycles,
+#          GRBM_GUI_ACTIVE (the clock the run held)
+#   misc   SALU / LDS / VMEM / SMEM instruction counts and the wait buckets
+#   fetch  FETCH_SIZE ; write  WRITE_SIZE
+# and, once per call, scripts/valu_cost (cycles per wave-instruction of each class).
+# Each step has its own time limit; the script stops at the first failure.
 set -eu
-tag=$1
+tag=$1; shift
+work=${*:-pt bdpt}
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 out=gpurun_out/prof_$tag
 mkdir -p "$out"
-PT="python bench.py --mode pt --steps 1 --warmup 1 --no-cpu"
-BD="python bench.py --mode bdpt --steps 1 --warmup 0 --no-cpu"
 run() {  # name timeout args...
   local name=$1 to=$2; shift 2
-  echo "=== $name"
+  echo "=== $name $(date +%T)"
   timeout -k 10 "$to" "$@" > "$out/$name.log" 2>&1 || { echo "step $name failed rc=$?"; tail -5 "$out/$name.log"; exit 1; }
 }
-run pt_kt 180 rocprofv3 --kernel-trace --stats -d "$out/pt_kt" -o run --output-format csv -- $PT
-run bdpt_kt 240 rocprofv3 --kernel-trace --stats -d "$out/bdpt_kt" -o run --output-format csv -- $BD
-run pt_fetch 180 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$out/pt_fetch" -o run --output-format csv -- $PT
-run pt_write 180 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$out/pt_write" -o run --output-format csv -- $PT
-run bdpt_fetch 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$out/bdpt_fetch" -o run --output-format csv -- $BD
-run bdpt_write 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$out/bdpt_write" -o run --output-format csv -- $BD
-run pt_sq 180 rocprofv3 --pmc SQ_INSTS_VALU,SQ_ACTIVE_INST_VALU,SQ_WAVE_CYCLES,SQ_BUSY_CYCLES,SQ_INSTS_SALU,SQ_INSTS_LDS,SQ_WAIT_INST_ANY,SQ_WAVES --kernel-trace -d "$out/pt_sq" -o run --output-format csv -- $PT
-echo "=== done"
+P1=SQ_INSTS_VALU,SQ_INSTS_VALU_ADD_F32,SQ_INSTS_VALU_MUL_F32,SQ_INSTS_VALU_FMA_F32,SQ_INSTS_VALU_TRANS_F32,SQ_INSTS_VALU_ADD_F64,SQ_INSTS_VALU_MUL_F64,SQ_INSTS_VALU_FMA_F64
+P2=SQ_INSTS_VALU_TRANS_F64,SQ_INSTS_VALU_INT32,SQ_INSTS_VALU_INT64,SQ_INSTS_VALU_CVT,SQ_ACTIVE_INST_VALU,SQ_WAVE_CYCLES,SQ_BUSY_CYCLES,SQ_WAIT_INST_ANY,GRBM_GUI_ACTIVE,GRBM_COUNT
+P3=SQ_INSTS_SALU,SQ_INSTS_LDS,SQ_INSTS_VMEM_RD,SQ_INSTS_VMEM_WR,SQ_INSTS_SMEM,SQ_WAIT_ANY,SQ_ACTIVE_INST_ANY,SQ_WAVES
+run valu_cost 120 scripts/valu_cost
+for w in $work; do
+  case $w in
+    pt)   B="python bench.py --mode pt --steps 1 --warmup 1 --no-cpu" ;;
+    bdpt) B="python bench.py --mode bdpt --steps 1 --warmup 0 --spp 32 --no-cpu" ;;
+    c5)   B="python bench.py --mode c5 --steps 1 --warmup 0 --spp 32 --no-cpu" ;;
+    pti)  B="python bench.py --mode pti --steps 1 --warmup 0 --spp 64 --no-cpu" ;;
+    *) echo "unknown workload $w"; exit 2 ;;
+  esac
+  run ${w}_kt 240 rocprofv3 --kernel-trace --stats -d "$out/${w}_kt" -o run --output-format csv -- $B
+  run ${w}_valu1 180 rocprofv3 --pmc $P1 --kernel-trace -d "$out/${w}_valu1" -o run --output-format csv -- $B
+  run ${w}_valu2 180 rocprofv3 --pmc $P2 --kernel-trace -d "$out/${w}_valu2" -o run --output-format csv -- $B
+  run ${w}_misc 180 rocprofv3 --pmc $P3 --kernel-trace -d "$out/${w}_misc" -o run --output-format csv -- $B
+  run ${w}_fetch 180 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$out/${w}_fetch" -o run --output-format csv -- $B
+  run ${w}_write 180 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$out/${w}_write" -o run --output-format csv -- $B
+done
+echo "=== done $(date +%T)"

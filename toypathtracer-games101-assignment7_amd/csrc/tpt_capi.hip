@@ -650,7 +650,11 @@ int64_t shard_count(int64_t npix, int64_t begin, int64_t stride) {
 // Launch the integration kernel for `count` pixels; rows/splat are device buffers.
 int launch(tpt_ctx* c, int mode, int spp, int64_t begin, int64_t stride, int64_t count, const int64_t* dlist,
            float* drows, float* dsplat, tpt_stats* st) {
-    if (count <= 0) return TPT_OK;
+    if (st) std::memset(st, 0, sizeof(*st));  // an empty shard or list reports zeros
+    if (count <= 0) {  // nothing to trace; the caller's memsets still complete before returning
+        HIP_TRY(c, hipStreamSynchronize(c->stream));
+        return TPT_OK;
+    }
     const int64_t blocks = (count + kBlock - 1) / kBlock;
     HIP_TRY(c, hipMemsetAsync(c->counters, 0, sizeof(unsigned long long) * 32, c->stream));
     HIP_TRY(c, hipEventRecord(c->ev0, c->stream));

@@ -280,6 +280,19 @@ int build_host_scene(const tpt_scene_desc* d, HostScene& hs, std::string& err) {
         err = "invalid scene description";
         return TPT_E_INVALID;
     }
+    // The reference's camera and splat code assume width >= height:
+    //  * the aspect ratio is an integer division, `float imageAspectRatio = width /
+    //    height` (SceneRenderingHelper.cpp:17, :25), which is 0 when width < height,
+    //    so RayToUV divides by zero (:26) and DrawToImage converts inf to int (:35-36);
+    //  * DrawToImage writes `buffer[ix + height * iy]` (SceneRenderingHelper.cpp:50),
+    //    which for height > width runs past the W*H splat buffer -- in the reference a
+    //    heap overflow, on the GPU an out-of-bounds float atomic into HBM.
+    // Such frames are refused instead of reproducing undefined behaviour.
+    if (d->height > d->width) {
+        err = "height > width is not supported: the reference's integer aspect ratio (SceneRenderingHelper.cpp:17) "
+              "is 0 and its splat index ix + height*iy (SceneRenderingHelper.cpp:50) overruns the frame";
+        return TPT_E_UNSUPPORTED;
+    }
     for (int i = 0; i < d->num_materials; ++i) {
         const tpt_material& m = d->materials[i];
         if (m.type < 0 || m.type > 2) { err = "invalid material type"; return TPT_E_INVALID; }
