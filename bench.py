@@ -173,13 +173,19 @@ def valu_roofline(key, kernel_ms, shard_frac):
     achieved = cyc / (ms / 1e3) / 1e9
     clk = model.get("clock_mhz") or MAX_CLOCK_MHZ
     peak = N_SIMD * clk / 1e3
-    return {"bound": "valu", "achieved": round(achieved, 1), "peak": round(peak, 1), "unit": "G SIMD-cycles/s",
+    t = _load_json("traffic.json").get(key)
+    out = {"bound": "valu", "achieved": round(achieved, 1), "peak": round(peak, 1), "unit": "G SIMD-cycles/s",
             "frac": round(achieved / peak, 4), "frac_at_2400mhz": round(achieved / (N_SIMD * MAX_CLOCK_MHZ / 1e3), 4),
-            "traffic": model.get("hbm_bytes_per_launch"), "kernel": model["kernel"], "kernel_ms": round(ms, 3),
+            "traffic": float(t["bytes_per_launch"]) * shard_frac if t else None,
+            "kernel": model["kernel"], "kernel_ms": round(ms, 3),
             "issue_cycles_per_launch": round(cyc), "clock_mhz": clk,
             "source": model.get("source"),
             "note": "VALU issue cycles per launch (PMC class counts x measured cycles per wave-instruction, "
-                    "profiles/valu_model.json) / live kernel time / (1,024 SIMDs x the profiled clock)"}
+                    "profiles/valu_model.json) / live kernel time / (1,024 SIMDs x the profiled clock); "
+                    "traffic = measured memory-side bytes per launch (profiles/traffic.json)"}
+    if len(model.get("per_kernel", {})) > 1:  # BDPT: a sequence of kernels on two streams
+        out["per_kernel_profiled"] = model["per_kernel"]
+    return out
 
 
 def hbm_model(scene, mode, kernel_ms, samples, traffic_key):
@@ -294,7 +300,11 @@ def main():
     r = Runner(a)
     info = cpu_info()
     want_cpu = not a.no_cpu and r.world == 1 and r.rank == 0
-    threads = a.cpu_threads or info["affinity"]
+    # every CPU this process may use: the affinity mask, capped by the cgroup's CPU
+    # quota (the GPU box gives each job a 16-CPU share of a 256-CPU host; more threads
+    # than that only time-slice)
+    threads = a.cpu_threads or (min(info["affinity"], max(1, int(info["cgroup_cpus"])))
+                                if info["cgroup_cpus"] else info["affinity"])
     keys = [a.mode] if a.mode else ["pt", "bdpt"] + ([] if a.no_c5 else ["c5"])
     lines = {}
     for k in keys:

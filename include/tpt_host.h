@@ -17,7 +17,8 @@ extern "C" {
 
 typedef struct tpt_preset tpt_preset;
 
-/* name: "silver" | "standard" | "refractive_ball" | "occlusion" |
+/* name: "silver" | "standard" | "refractive_ball" | "occlusion" | "multi_light" |
+ *       "emissive_sphere" | "background" |
  *       "smooth_dielectric" | "bunny".  Returns 0 or TPT_E_INVALID. */
 int tpt_preset_load(const char* models_dir, const char* name, int32_t width, int32_t height, tpt_preset** out);
 const tpt_scene_desc* tpt_preset_desc(const tpt_preset* p);

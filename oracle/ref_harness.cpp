@@ -66,13 +66,20 @@ Material* keep(Material* m) { g.mats.push_back(m); return m; }
 extern "C" {
 
 // Build one of the named presets.  Returns 0 on success, -1 on an unknown preset.
+// Edge-case presets (builder-declared, VERDICT r1 "Missing" #4), all on the standard
+// box: "multi_light" adds the reference's light2.obj / light3.obj as two more
+// emitters (PathTracer.cpp:82 loops over all of them); "emissive_sphere" adds a
+// glowing Sphere ahead of the light, so it is m_emissionObjects[0] (BDPT.cpp:287
+// starts every light path on it: Sphere::Sample, Sphere.cpp:48-55); "background"
+// keeps Scene.hpp:23's default backgroundColor instead of main.cpp:51's 0 (read by
+// BDPT.cpp:182 and BDPT.hpp:124).
 int ref_setup(const char* models_dir, const char* preset, int width, int height) {
     std::string dir(models_dir);
     std::string p(preset);
     g = Preset();
     Scene* scene = new Scene(width, height);
     scene->eyePos = Vector3f(278, 278, -800);
-    scene->backgroundColor = 0.0f;
+    if (p != "background") scene->backgroundColor = 0.0f;
     Material* red = keep(new Material(Dieletric, Vector3f(0.0f)));
     red->Kd = Vector3f(0.63f, 0.065f, 0.05f);
     Material* green = keep(new Material(Dieletric, Vector3f(0.0f)));
@@ -94,9 +101,13 @@ int ref_setup(const char* models_dir, const char* preset, int width, int height)
     glass->ior_d = 1.5f;
     glass->SetSmoothness(.9f);
 
+    Material* lightball = keep(new Material(Dieletric, Vector3f(3.0f, 2.4f, 1.5f)));
+    lightball->Kd = Vector3f(0.65f);
+
     Material* boxes = nullptr;
     if (p == "silver") boxes = silver;
-    else if (p == "standard" || p == "refractive_ball" || p == "occlusion" || p == "smooth_dielectric" || p == "bunny")
+    else if (p == "standard" || p == "refractive_ball" || p == "occlusion" || p == "smooth_dielectric" || p == "bunny" ||
+             p == "multi_light" || p == "emissive_sphere" || p == "background")
         boxes = white;
     else return -1;
 
@@ -117,7 +128,16 @@ int ref_setup(const char* models_dir, const char* preset, int width, int height)
         scene->Add(mesh("tallbox.obj", boxes));
         scene->Add(mesh("left.obj", red));
         scene->Add(mesh("right.obj", green));
+        if (p == "emissive_sphere") {
+            Sphere* s = new Sphere(Vector3f(420.0f, 60.0f, 150.0f), 60.0f, lightball);
+            g.objs.push_back(s);
+            scene->Add(s);
+        }
         scene->Add(mesh("light.obj", light));
+        if (p == "multi_light") {
+            scene->Add(mesh("light2.obj", light));
+            scene->Add(mesh("light3.obj", light));
+        }
         if (p == "refractive_ball") {
             Sphere* s = new Sphere(Vector3f(278.0f, 278.0f, 200.0f), 50.0f, glass);
             g.objs.push_back(s);

@@ -1165,7 +1165,8 @@ static Scene* preset(const std::string& dir, const std::string& p, int w, int h)
     Scene* sc = new Scene();
     sc->width = w; sc->height = h;
     sc->eye = V3(278, 278, -800);
-    sc->bg = V3(0.0f);
+    // main.cpp:51 sets the background to 0; "background" keeps Scene.hpp:23's default
+    sc->bg = p == "background" ? V3(0.235294f, 0.67451f, 0.843137f) : V3(0.0f);
     auto mat = [&](int type, V3 e) { Material m; m.type = type; m.emission = e; m.kd = V3(0.5f, 0.5f, 0.5f); sc->mats.push_back(m); return (int)sc->mats.size() - 1; };
     int red = mat(DIELETRIC, V3(0.0f)); sc->mats[red].kd = V3(0.63f, 0.065f, 0.05f);
     int green = mat(DIELETRIC, V3(0.0f)); sc->mats[green].kd = V3(0.14f, 0.45f, 0.091f);
@@ -1179,9 +1180,11 @@ static Scene* preset(const std::string& dir, const std::string& p, int w, int h)
     sc->mats[silver].ior_m_k = V3(4.8025f, 3.4101f, 2.8545f);
     sc->mats[silver].rough = smooth_to_rough(1.f);
     int glass = mat(TRANSPARENT, V3(0.0f)); sc->mats[glass].ior_d = 1.5f; sc->mats[glass].rough = smooth_to_rough(.9f);
+    int lightball = mat(DIELETRIC, V3(3.0f, 2.4f, 1.5f)); sc->mats[lightball].kd = V3(0.65f);
     int boxes;
     if (p == "silver") boxes = silver;
-    else if (p == "standard" || p == "refractive_ball" || p == "occlusion" || p == "smooth_dielectric" || p == "bunny") boxes = white;
+    else if (p == "standard" || p == "refractive_ball" || p == "occlusion" || p == "smooth_dielectric" || p == "bunny" ||
+             p == "multi_light" || p == "emissive_sphere" || p == "background") boxes = white;
     else { delete sc; return nullptr; }
     auto mesh = [&](const char* f, int m) {
         std::vector<V3> soup;
@@ -1195,7 +1198,11 @@ static Scene* preset(const std::string& dir, const std::string& p, int w, int h)
         ok &= mesh("light.obj", light); ok &= mesh("bunny_cornell.obj", white);
     } else {
         ok &= mesh("floor.obj", boxes); ok &= mesh("shortbox.obj", boxes); ok &= mesh("tallbox.obj", boxes);
-        ok &= mesh("left.obj", red); ok &= mesh("right.obj", green); ok &= mesh("light.obj", light);
+        ok &= mesh("left.obj", red); ok &= mesh("right.obj", green);
+        // "emissive_sphere": the glowing ball is m_emissionObjects[0] (BDPT.cpp:287)
+        if (p == "emissive_sphere") add_sphere(*sc, V3(420.0f, 60.0f, 150.0f), 60.0f, lightball);
+        ok &= mesh("light.obj", light);
+        if (p == "multi_light") { ok &= mesh("light2.obj", light); ok &= mesh("light3.obj", light); }
         if (p == "refractive_ball") add_sphere(*sc, V3(278.0f, 278.0f, 200.0f), 50.0f, glass);
         if (p == "occlusion") ok &= mesh("lightocculuder.obj", white);
     }

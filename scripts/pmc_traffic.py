@@ -40,7 +40,7 @@ def main():
     ap.add_argument("fetch_csv")
     ap.add_argument("write_csv")
     ap.add_argument("--note", default="")
-    ap.add_argument("--frames", type=int, default=None,
+    ap.add_argument("--frames", type=float, default=None,
                     help="sum every matching dispatch and divide by this many frames (BDPT: the "
                          "wavefront sequence of one frame is the 'launch')")
     a = ap.parse_args()

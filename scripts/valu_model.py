@@ -10,10 +10,10 @@ KERNEL    substring of the kernel names to sum (tpt_pt_kernel, tpt_bdpt_)
           per-launch figures are totals / frames
 --scale   multiply per-frame counts (a BDPT profile at 32 spp scaled to the 256-spp
           frame bench.py times: 8)
---waves   waves per SIMD the kernel runs at; picks the cost column of valu_cost.log
+--waves   valu_cost.log column (default 8 waves per SIMD: the issue-saturated rate)
 
 Issue cycles = sum over classes of (wave-instruction count x cycles per wave-
-instruction), the costs measured by scripts/valu_cost.hip on the same box:
+instruction), the costs measured by scripts/valu_cost.hip on the same box (costs()):
   ADD/MUL/FMA_F32 -> v_add/v_mul/v_fma_f32     ADD/MUL/FMA_F64 -> v_add/v_mul/v_fma_f64
   TRANS_F32 -> mean(v_rcp_f32, v_sqrt_f32)     TRANS_F64 -> mean(v_rcp_f64, v_sqrt_f64)
   INT32 -> v_add_u32   INT64 -> v_lshlrev_b64   CVT -> (v_cvt_f32_f64 + v_cvt_f64_f32) / 2
@@ -34,13 +34,16 @@ CLASSES = ["ADD_F32", "MUL_F32", "FMA_F32", "TRANS_F32", "ADD_F64", "MUL_F64", "
 
 
 def costs(log, waves):
+    """Cycles per wave-instruction of each class on one SIMD: valu_cost's event-time
+    figure at `waves` waves per SIMD (default 8: issue-saturated).  It includes the
+    benchmark's loop overhead (3 SALU per 32 VALU), so it errs high by ~0.2 cycle."""
     c = {}
     for line in open(log):
         line = line.strip()
         if line.startswith("{"):
             r = json.loads(line)
             if r["waves_per_simd"] == waves:
-                c[r["inst"]] = r["cycles_per_wave_inst"] / (2.0 if "+" in r["inst"] else 1.0)
+                c[r["inst"]] = r["cycles_per_wave_inst_event"] / (2.0 if "+" in r["inst"] else 1.0)
     m = statistics.mean
     return {"ADD_F32": c["v_add_f32"], "MUL_F32": c["v_mul_f32"], "FMA_F32": c["v_fma_f32"],
             "TRANS_F32": m([c["v_rcp_f32"], c["v_sqrt_f32"]]), "ADD_F64": c["v_add_f64"], "MUL_F64": c["v_mul_f64"],
@@ -91,8 +94,9 @@ def main():
     ap.add_argument("kernel")
     ap.add_argument("--frames", type=float, default=1.0)
     ap.add_argument("--scale", type=float, default=1.0)
-    ap.add_argument("--waves", type=int, default=4)
+    ap.add_argument("--waves", type=int, default=8, help="valu_cost column (8: issue-saturated)")
     ap.add_argument("--note", default="")
+    ap.add_argument("--source", default=None, help="committed summary the figures come from (profiles/...)")
     a = ap.parse_args()
     cost = costs(os.path.join(a.prof_dir, "valu_cost.log"), a.waves)
     p = lambda s: os.path.join(a.prof_dir, "%s_%s" % (a.workload, s))  # noqa: E731
@@ -117,14 +121,15 @@ def main():
              "valu_insts_per_launch": round(cnt.get("SQ_INSTS_VALU", 0) * f),
              "class_insts_per_launch": {k: round(v * f) for k, v in classes.items()},
              "other_insts_per_launch": round(other * f),
-             "cycles_per_wave_inst": {k: round(v, 3) for k, v in cost.items()}, "waves_per_simd": a.waves,
+             "cycles_per_wave_inst": {k: round(v, 3) for k, v in cost.items()},
+             "cost_waves_per_simd": a.waves,
              "clock_mhz": round(clock_mhz, 1) if clock_mhz else None,
              "sq_busy_cycles_per_se": round(busy / 32.0 / a.frames) if busy else None,
              "kernel_ms_per_launch_kt": round(ns_kt * 1e-6 * f, 3),
              "valu_frac_in_profile": round(cyc / (1024 * clock_mhz * 1e6 * ns2 * 1e-9), 4) if ns2 and clock_mhz else None,
              "active_inst_valu_quad": cnt.get("SQ_ACTIVE_INST_VALU"), "wave_cycles_quad": cnt.get("SQ_WAVE_CYCLES"),
              "wait_inst_any_quad": cnt.get("SQ_WAIT_INST_ANY"),
-             "per_kernel": per, "source": os.path.relpath(a.prof_dir, ROOT), "note": a.note}
+             "per_kernel": per, "source": a.source or os.path.relpath(a.prof_dir, ROOT), "note": a.note}
     out = os.path.join(ROOT, "profiles", "valu_model.json")
     db = json.load(open(out)) if os.path.exists(out) else {}
     db[a.key] = entry

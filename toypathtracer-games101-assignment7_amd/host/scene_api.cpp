@@ -189,12 +189,16 @@ void Renderer::Render(std::string out, const Scene& scene, int spp, int thread_c
 }
 
 // main.cpp:49-103 (+ SURVEY §8(d) variants).  Materials and Add order as in the
-// reference; the smooth_dielectric preset declares white's smoothness = 0.7.
+// reference; the smooth_dielectric preset declares white's smoothness = 0.7.  Edge
+// cases: "multi_light" (+ light2.obj, light3.obj as emitters), "emissive_sphere" (a
+// glowing Sphere as m_emissionObjects[0]), "background" (Scene.hpp:23's default
+// backgroundColor kept).
 bool BuildPresetScene(const std::string& dir, const std::string& p, Scene& scene) {
     static std::vector<Material*> keep_m;
     static std::vector<Object*> keep_o;
     scene.eyePos = Vector3f(278, 278, -800);
-    scene.backgroundColor = 0.0f;
+    // main.cpp:51 sets the background to 0; "background" keeps Scene.hpp:23's default
+    scene.backgroundColor = p == "background" ? Vector3f(0.235294f, 0.67451f, 0.843137f) : Vector3f(0.0f);
     auto M = [&](Material* m) { keep_m.push_back(m); return m; };
     Material* red = M(new Material(Dieletric, Vector3f(0.0f)));
     red->Kd = Vector3f(0.63f, 0.065f, 0.05f);
@@ -214,9 +218,12 @@ bool BuildPresetScene(const std::string& dir, const std::string& p, Scene& scene
     Material* glass = M(new Material(Transparent));
     glass->ior_d = 1.5f;
     glass->SetSmoothness(.9f);
+    Material* lightball = M(new Material(Dieletric, Vector3f(3.0f, 2.4f, 1.5f)));
+    lightball->Kd = Vector3f(0.65f);
     Material* boxes = nullptr;
     if (p == "silver") boxes = silver;
-    else if (p == "standard" || p == "refractive_ball" || p == "occlusion" || p == "smooth_dielectric" || p == "bunny")
+    else if (p == "standard" || p == "refractive_ball" || p == "occlusion" || p == "smooth_dielectric" || p == "bunny" ||
+             p == "multi_light" || p == "emissive_sphere" || p == "background")
         boxes = white;
     else return false;
     bool ok = true;
@@ -238,7 +245,16 @@ bool BuildPresetScene(const std::string& dir, const std::string& p, Scene& scene
         mesh("tallbox.obj", boxes);
         mesh("left.obj", red);
         mesh("right.obj", green);
+        if (p == "emissive_sphere") {  // the glowing ball is m_emissionObjects[0] (BDPT.cpp:287)
+            Sphere* s = new Sphere(Vector3f(420.0f, 60.0f, 150.0f), 60.0f, lightball);
+            keep_o.push_back(s);
+            scene.Add(s);
+        }
         mesh("light.obj", light);
+        if (p == "multi_light") {
+            mesh("light2.obj", light);
+            mesh("light3.obj", light);
+        }
         if (p == "refractive_ball") {
             Sphere* s = new Sphere(Vector3f(278.0f, 278.0f, 200.0f), 50.0f, glass);
             keep_o.push_back(s);
