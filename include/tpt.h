@@ -17,6 +17,8 @@
  *   Scene::BuildBVH / BVHAccel ctor / MeshTriangle ctor
  *                                               Scene.cpp:11-19, BVH.cpp:5-99, Triangle.cpp:32-75
  *     -> tpt_upload_scene (BVH built on the host, flattened, copied to HBM)
+ *   Renderer::Render's std::async workers + splat merge   Renderer.cpp:86-114
+ *     -> tpt_multi_* / tpt_render_multi (pixel shards per GPU + one RCCL reduce)
  *
  * Conventions: every call is synchronous and returns 0 on
  * success or a negative TPT_E* code; no C++ exception crosses the ABI; the
@@ -160,6 +162,28 @@ int tpt_intersect(tpt_ctx* ctx, const float* rays, int64_t n, int32_t cull, floa
 
 /* Camera scale (SceneRenderingHelper.cpp:12-14), computed on the host. */
 float tpt_camera_scale(double fov);
+
+/* ---- multi-GPU (one process, the GPUs of one node) ---------------------------
+ * Replaces Renderer::Render's worker split and splat merge (Renderer.cpp:86-114)
+ * across devices instead of threads: device r of n renders the pixel shard
+ * i = r, r + n, ... (Renderer.cpp:38's interleave) with its own context, then ONE
+ * RCCL reduce (sum, fp32, over xGMI) of every device's [rgb; splat] buffer onto the
+ * first device.  Radiance shards are disjoint, so the frame is bit-identical to one
+ * GPU; splats (already scaled by 1/spp per device, Renderer.cpp:59) are summed as the
+ * reference sums its per-thread buffers (:98-114).  RCCL is loaded when the group is
+ * created; TPT_E_UNSUPPORTED if it cannot be. */
+typedef struct tpt_multi tpt_multi;
+
+/* devices: ngpu HIP device ids (NULL: 0 .. ngpu-1); one tpt_ctx per device. */
+int tpt_multi_create(int ngpu, const int* devices, tpt_multi** out);
+void tpt_multi_destroy(tpt_multi* m);
+const char* tpt_multi_last_error(const tpt_multi* m);
+/* tpt_upload_scene on every device. */
+int tpt_multi_upload_scene(tpt_multi* m, const tpt_scene_desc* desc);
+/* As tpt_render for the whole frame (params->pixel_begin 0, pixel_stride 1: the group
+ * shards it).  stats sums pixels / samples / bounces over devices; kernel_ms is the
+ * slowest device's. */
+int tpt_render_multi(tpt_multi* m, const tpt_render_params* params, float* rgb, float* splat, tpt_stats* stats);
 
 #ifdef __cplusplus
 }

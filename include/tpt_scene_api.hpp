@@ -104,7 +104,7 @@ public:
 
 struct RenderOptions {
     int device = 0;              // first HIP device
-    int gpus = 1;                // >1: pixel-sharded multi-GPU (one process per GPU: see bench.py)
+    int gpus = 1;                // >1: devices device .. device+gpus-1, pixel-sharded, one RCCL reduce (tpt_render_multi)
     std::string float_dump;      // optional raw fp32 W*H*3 dump (parity artefact)
     bool quiet = false;
     bool pt_indirect = false;    // PathTrace with the indirect bounce (TPT_MODE_PT_INDIRECT); off by default

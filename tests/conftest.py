@@ -25,3 +25,13 @@ def golden(name):
 def bits(a):
     import numpy as np
     return np.ascontiguousarray(a, np.float32).view(np.uint32)
+
+# reference edge cases (tests/golden/make_golden.py edge): name -> (preset, width, height)
+EDGE = {"multi_light": ("multi_light", 784, 784), "emissive_sphere": ("emissive_sphere", 784, 784),
+        "background": ("background", 784, 784), "standard_1280x960": ("standard", 1280, 960)}
+
+
+def blocks(img, b=8):
+    import numpy as np
+    h, w = img.shape[:2]
+    return img.reshape(h // b, b, w // b, b, 3).astype(np.float64).mean((1, 3)).astype(np.float32)

@@ -16,8 +16,20 @@ Contents (all float32 unless noted):
   pt_indirect.npz       TPT_MODE_PT_INDIRECT: per-pixel replay through the reference's
                         PathTrace compiled without the `break` at PathTracer.cpp:109
                         (oracle/build_ref.sh), spp 1 and 8, radiance + outBounces sums
+  edge_<case>.npz       the reference's edge cases (VERDICT r1 Missing #4):
+                        multi_light (three emitters, two of them coplanar and
+                        overlapping: PathTracer.cpp:82's loop, closest-hit ties),
+                        emissive_sphere (a Sphere as m_emissionObjects[0]: Sphere::Sample,
+                        Sphere.cpp:48-55), background (Scene.hpp:23's default colour,
+                        BDPT.cpp:182 / BDPT.hpp:124), standard_1280x960 (Scene.hpp:19-20's
+                        default frame: integer aspect 1, splat index ix + height*iy,
+                        SceneRenderingHelper.cpp:17, :50).  Each: closest hits, PT 1/16 spp
+                        and BDPT 4 spp per-pixel replay (+ splats, bounces), PT-indirect
+                        4 spp, and a real Renderer::Render frame (PT 4 spp -j8, BDPT 1 spp -j1)
+                        as 8x8 block means
 
     python tests/golden/make_golden.py indirect   # only pt_indirect.npz
+    python tests/golden/make_golden.py edge       # only edge_<case>.npz
 """
 import os
 import sys
@@ -75,9 +87,9 @@ def material_cases(rng, n):
     return cases
 
 
-def pixel_set(seed, n):
+def pixel_set(seed, n, w=W, h=H):
     rng = np.random.default_rng(seed)
-    return np.sort(rng.choice(W * H, n, replace=False)).astype(np.int64)
+    return np.sort(rng.choice(w * h, n, replace=False)).astype(np.int64)
 
 
 def ray_set(rng, n):
@@ -92,6 +104,51 @@ def ray_set(rng, n):
     d[k:] = unit(rng, n - k)
     d /= np.linalg.norm(d, axis=1, keepdims=True)
     return np.concatenate([o, d.astype(np.float32)], 1).astype(np.float32)
+
+
+# name -> (preset, width, height)
+EDGE = {"multi_light": ("multi_light", 784, 784), "emissive_sphere": ("emissive_sphere", 784, 784),
+        "background": ("background", 784, 784), "standard_1280x960": ("standard", 1280, 960)}
+
+
+def light_rays(rng, n):
+    """Rays from inside the box toward the ceiling-light plane (y = 548.7) over all
+    three light quads, two of which overlap (light.obj / light3.obj): tie order."""
+    o = rng.uniform([20, 20, 20], [540, 500, 540], size=(n, 3)).astype(np.float32)
+    t = np.stack([rng.uniform(10, 500, n), np.full(n, 548.7), rng.uniform(227, 332, n)], 1).astype(np.float32)
+    d = t - o
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    return np.concatenate([o, d.astype(np.float32)], 1).astype(np.float32)
+
+
+def blocks(img, b=8):
+    h, w = img.shape[:2]
+    return img.reshape(h // b, b, w // b, b, 3).astype(np.float64).mean((1, 3)).astype(np.float32)
+
+
+def edge():
+    rng = np.random.default_rng(20261016)
+    for k, (name, (p, w, h)) in enumerate(EDGE.items()):
+        R = Reference(p, w, h)
+        out = {"width": np.int32(w), "height": np.int32(h)}
+        rays = np.concatenate([ray_set(rng, 1536), light_rays(rng, 512)])
+        out["rays"] = rays
+        out["hits"] = np.stack([R.intersect(rays, c) for c in (0, 1, 2)])
+        pix = pixel_set(300 + k, 2048, w, h)
+        out["pix"] = pix
+        out["pt1"], _, _ = R.trace_pixels(0, 1, pix)
+        out["pt16"], _, _ = R.trace_pixels(0, 16, pix)
+        bpix = pix[::8]
+        out["bpix"] = bpix
+        bd4, splat, bounces = R.trace_pixels(1, 4, bpix, want_splat=True)
+        nz = np.nonzero(splat.reshape(-1))[0].astype(np.int64)
+        out["bdpt4"], out["bdpt4_bounces"] = bd4, bounces
+        out["splat_idx"], out["splat_val"] = nz, splat.reshape(-1)[nz]
+        out["pti4"], _, out["pti4_bounces"] = R.trace_pixels(2, 4, pix[::4])
+        out["pt4_blocks"] = blocks(R.render(0, 4, threads=8))
+        out["bdpt1_blocks"] = blocks(R.render(1, 1, threads=1))
+        np.savez_compressed(os.path.join(HERE, "edge_%s.npz" % name), **out)
+        print("edge", name, "done", flush=True)
 
 
 def indirect():
@@ -111,6 +168,8 @@ def main():
         sys.exit("oracle/_ref/libref.so missing: run oracle/build_ref.sh first")
     if sys.argv[1:] == ["indirect"]:
         return indirect()
+    if sys.argv[1:] == ["edge"]:
+        return edge()
     rng = np.random.default_rng(20261015)
     R = Reference("standard")
 
@@ -157,6 +216,7 @@ def main():
                         pt16_crop=img_pt[360:424, 360:424], bdpt2_blocks=blocks(img_bd),
                         bdpt2_crop=img_bd[360:424, 360:424], crop_origin=np.array([360, 360]))
     indirect()
+    edge()
     print("done")
 
 

@@ -1,4 +1,6 @@
-// Minimal C++ caller of the C ABI (diagnostics; prints a backtrace on SIGSEGV).
+// Minimal C++ caller of the C ABI: preset -> upload -> closest hit -> 1-spp PT frame.
+// Built by tests/test_abi.py::test_abi_smoke_builds, run by tests/test_gpu_parity.py::test_cli_and_abi_smoke.
+// Prints a backtrace on SIGSEGV.
 #include <execinfo.h>
 #include <signal.h>
 #include <unistd.h>
@@ -24,6 +26,7 @@ int main(int argc, char** argv) {
     if (rc) return 1;
     rc = tpt_upload_scene(c, tpt_preset_desc(p));
     std::printf("upload %d %s\n", rc, tpt_last_error(c)); std::fflush(stdout);
+    if (rc) return 1;
     float ray[6] = {278, 278, -800, 0, 0, 1}, out[8];
     rc = tpt_intersect(c, ray, 1, TPT_CULL_BACK, out);
     std::printf("intersect %d %s hit=%g x=%g %g %g prim=%g\n", rc, tpt_last_error(c), out[0], out[1], out[2], out[3], out[7]);
@@ -33,6 +36,7 @@ int main(int argc, char** argv) {
     rc = tpt_render(c, &rp, rgb.data(), nullptr, &st);
     double s = 0; for (float v : rgb) s += v;
     std::printf("render %d %s sum=%g kernel_ms=%g\n", rc, tpt_last_error(c), s, st.kernel_ms);
+    if (rc) return 1;
     tpt_destroy(c);
     tpt_preset_free(p);
     return 0;

@@ -80,3 +80,31 @@ def test_film_output(tmp_path):
     # SceneRenderingHelper.cpp:62-64
     want = (255 * np.power(np.clip(rgb, 0, 1), np.float32(0.6))).astype(np.uint8)
     assert np.abs(px.astype(int) - want.astype(int)).max() <= 1
+
+
+NATIVE = os.path.join(ROOT, "tests", "native")
+
+
+@pytest.mark.skipif(not os.path.exists("/root/reference/main.cpp"), reason="reference sources not present")
+def test_reference_main_compiles_against_drop_in():
+    """The reference's own, unmodified main.cpp (main.cpp:36-152: its hard-coded scene,
+    tryParseArg flags and Renderer::Render call) compiles against
+    include/tpt_scene_api.hpp and links to libtpt.so (tests/native/build_dropin.sh)."""
+    import subprocess
+    subprocess.check_call([os.path.join(NATIVE, "build_dropin.sh")])
+    exe = os.path.join(NATIVE, "build", "ref_main_tpt")
+    assert os.access(exe, os.X_OK)
+    deps = subprocess.check_output(["ldd", exe]).decode()
+    assert "libtpt.so" in deps and "not found" not in deps
+
+
+def test_abi_smoke_builds():
+    """A plain C++ caller of the C ABI (tests/native/abi_smoke.cpp) compiles with g++
+    against include/ and links to libtpt.so; the GPU suite runs it."""
+    import subprocess
+    out = os.path.join(NATIVE, "build")
+    os.makedirs(out, exist_ok=True)
+    pkg = os.path.join(ROOT, "toypathtracer-games101-assignment7_amd")
+    subprocess.check_call(["g++", "-std=c++17", "-O1", os.path.join(NATIVE, "abi_smoke.cpp"), "-I", os.path.join(ROOT, "include"),
+                           "-L", pkg, "-ltpt", "-Wl,-rpath,$ORIGIN/../../../toypathtracer-games101-assignment7_amd",
+                           "-o", os.path.join(out, "abi_smoke")])

@@ -7,7 +7,7 @@
 import numpy as np
 import pytest
 
-from conftest import PRESETS, bits, golden
+from conftest import EDGE, PRESETS, bits, blocks, golden
 from oracle_bind import Oracle, Reference, ref_available
 
 
@@ -131,3 +131,35 @@ def test_traversal_counts_b_alg():
         nodes, tris = o.traversal_counts(mode, 1, pix)
         b = (nodes * 32 + tris * 48) / len(pix)
         assert abs(b / bench.B_ALG[("standard", name)] - 1) < 0.01, (name, b)
+
+
+@pytest.mark.parametrize("name", sorted(EDGE))
+def test_edge_cases(name):
+    """The reference's edge cases (golden edge_<name>.npz): several emitters with
+    coplanar overlapping quads, a sphere as emitter 0, a non-zero background, the
+    default 1280x960 frame.  Closest hits, PT / BDPT / PT-indirect per-pixel replay,
+    splats and bounce counts, and a full PT frame -- all bit-exact."""
+    g = golden("edge_%s.npz" % name)
+    p, w, h = EDGE[name]
+    o = Oracle(p, w, h)
+    for c in range(3):
+        assert eq_bits(o.intersect(g["rays"], c), g["hits"][c]), c
+    assert eq_bits(o.trace_pixels(0, 1, g["pix"])[0], g["pt1"])
+    assert eq_bits(o.trace_pixels(0, 16, g["pix"])[0], g["pt16"])
+    rgb, splat, b = o.trace_pixels(1, 4, g["bpix"], want_splat=True)
+    assert eq_bits(rgb, g["bdpt4"]) and np.array_equal(b, g["bdpt4_bounces"])
+    flat = splat.reshape(-1)
+    assert np.array_equal(np.nonzero(flat)[0], g["splat_idx"])
+    assert eq_bits(flat[g["splat_idx"]], g["splat_val"])
+    rgb, _, b = o.trace_pixels(2, 4, g["pix"][::4])
+    assert eq_bits(rgb, g["pti4"]) and np.array_equal(b, g["pti4_bounces"])
+    img, _ = o.render(0, 4, threads=8)
+    assert eq_bits(blocks(img), g["pt4_blocks"])
+
+
+def test_edge_full_frame_bdpt_1280x960():
+    """Renderer::Render's BDPT frame at 1280x960 (-j1): radiance plus splats that land
+    at the reference's `ix + height*iy` (SceneRenderingHelper.cpp:50)."""
+    g = golden("edge_standard_1280x960.npz")
+    img, _ = Oracle("standard", 1280, 960).render(1, 1, threads=1)
+    assert eq_bits(blocks(img), g["bdpt1_blocks"])

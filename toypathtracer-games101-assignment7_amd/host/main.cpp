@@ -1,7 +1,7 @@
 // tpt_render -- the reference's CLI (main.cpp:14-46, 147-148) on the GPU path.
 // Flags and defaults as the reference: -o output.jpg, -spp 1, -j 8 (accepted,
 // unused by the GPU path), -bdpt 1.  Additions: -scene <preset> (default
-// "silver" = main.cpp HEAD), -models <dir>, -dump <file.f32>, -device <n>,
+// "silver" = main.cpp HEAD), -models <dir>, -dump <file.f32>, -device <n>, -gpus <n>,
 // -pti 1 (PathTrace with the indirect bounce, TPT_MODE_PT_INDIRECT; with -bdpt 0).
 #include <iostream>
 #include <sstream>
@@ -36,6 +36,7 @@ int main(int argc, char** argv) {
     RenderOptions opt;
     opt.float_dump = tryParseArg(argc, argv, "-dump", std::string());
     opt.device = tryParseArg(argc, argv, "-device", 0);
+    opt.gpus = tryParseArg(argc, argv, "-gpus", 1);  // >1: tpt_render_multi over devices device..device+gpus-1
     opt.pt_indirect = tryParseArg(argc, argv, "-pti", 0) != 0;  // off by default
     Scene scene(784, 784);
     if (!BuildPresetScene(models, preset, scene)) {

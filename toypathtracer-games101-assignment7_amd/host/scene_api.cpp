@@ -138,29 +138,43 @@ void Renderer::Render(std::string out, const Scene& scene, int spp, int thread_c
     if (!opt.quiet) std::cout << "SPP: " << spp << "\n";
     Scene::Flat flat;
     scene.Flatten(flat);
-    tpt_ctx* ctx = nullptr;
-    int rc = tpt_create(opt.device, &ctx);
-    if (rc) { std::cerr << "tpt_create failed (" << rc << ")\n"; last_error = rc; return; }
-    rc = tpt_upload_scene(ctx, &flat.desc);
     const int64_t n = (int64_t)scene.width * scene.height * 3;
     framebuffer.assign(n, 0.0f);
     std::vector<float> splat(bdpt ? n : 0, 0.0f);
-    if (!rc) {
-        tpt_render_params p;
-        std::memset(&p, 0, sizeof(p));
-        p.spp = spp;
-        p.mode = bdpt ? TPT_MODE_BDPT : opt.pt_indirect ? TPT_MODE_PT_INDIRECT : TPT_MODE_PT;
-        p.pixel_begin = 0;
-        p.pixel_stride = 1;
-        rc = tpt_render(ctx, &p, framebuffer.data(), bdpt ? splat.data() : nullptr, &stats);
+    tpt_render_params p;
+    std::memset(&p, 0, sizeof(p));
+    p.spp = spp;
+    p.mode = bdpt ? TPT_MODE_BDPT : opt.pt_indirect ? TPT_MODE_PT_INDIRECT : TPT_MODE_PT;
+    p.pixel_begin = 0;
+    p.pixel_stride = 1;
+    int rc = TPT_OK;
+    std::string err;
+    if (opt.gpus > 1) {
+        // the reference's j std::async workers (Renderer.cpp:86-91) become opt.gpus
+        // devices; its thread-order splat merge (:98-114) one RCCL reduce
+        std::vector<int> devs;
+        for (int g = 0; g < opt.gpus; ++g) devs.push_back(opt.device + g);
+        tpt_multi* m = nullptr;
+        rc = tpt_multi_create(opt.gpus, devs.data(), &m);
+        if (rc) err = "tpt_multi_create failed (" + std::to_string(rc) + ")";
+        if (!rc) rc = tpt_multi_upload_scene(m, &flat.desc);
+        if (!rc) rc = tpt_render_multi(m, &p, framebuffer.data(), bdpt ? splat.data() : nullptr, &stats);
+        if (rc && m) err = tpt_multi_last_error(m);
+        tpt_multi_destroy(m);
+    } else {
+        tpt_ctx* ctx = nullptr;
+        rc = tpt_create(opt.device, &ctx);
+        if (rc) err = "tpt_create failed (" + std::to_string(rc) + ")";
+        if (!rc) rc = tpt_upload_scene(ctx, &flat.desc);
+        if (!rc) rc = tpt_render(ctx, &p, framebuffer.data(), bdpt ? splat.data() : nullptr, &stats);
+        if (rc && ctx) err = tpt_last_error(ctx);
+        tpt_destroy(ctx);
     }
     if (rc) {
-        std::cerr << "render failed: " << tpt_last_error(ctx) << "\n";
+        std::cerr << "render failed: " << err << "\n";
         last_error = rc;
-        tpt_destroy(ctx);
         return;
     }
-    tpt_destroy(ctx);
     if (bdpt) {
         if (!opt.quiet) std::cout << "Tracing finished, merge emission buffer\n";
         for (int64_t j = 0; j < n; ++j) framebuffer[j] += splat[j];

@@ -24,6 +24,7 @@ MODE_PT, MODE_BDPT = 0, 1
 MODE_PT_INDIRECT = 2  # PathTrace without the HEAD `break` (PathTracer.cpp:109); off by default
 CULL_BACK, CULL_FRONT, NO_CULL = 0, 1, 2
 PRESETS = ("silver", "standard", "refractive_ball", "occlusion", "smooth_dielectric", "bunny")
+EDGE_PRESETS = ("multi_light", "emissive_sphere", "background")
 
 
 class Material(ctypes.Structure):
@@ -58,6 +59,8 @@ class Stats(ctypes.Structure):
 # Every symbol declared in include/tpt.h and include/tpt_host.h.
 EXPORTS = ("tpt_create", "tpt_destroy", "tpt_last_error", "tpt_abi_version", "tpt_upload_scene", "tpt_render",
            "tpt_render_pixels", "tpt_render_device", "tpt_intersect", "tpt_camera_scale",
+           "tpt_multi_create", "tpt_multi_destroy", "tpt_multi_last_error", "tpt_multi_upload_scene",
+           "tpt_render_multi",
            "tpt_preset_load", "tpt_preset_desc", "tpt_preset_free", "tpt_save_image")
 
 _lib = None
@@ -92,6 +95,13 @@ def lib():
     L.tpt_preset_free.argtypes = [P]
     L.tpt_preset_free.restype = None
     L.tpt_save_image.argtypes = [P, ctypes.c_int32, ctypes.c_int32, ctypes.c_char_p]
+    L.tpt_multi_create.argtypes = [ctypes.c_int, P, ctypes.POINTER(P)]
+    L.tpt_multi_destroy.argtypes = [P]
+    L.tpt_multi_destroy.restype = None
+    L.tpt_multi_last_error.argtypes = [P]
+    L.tpt_multi_last_error.restype = ctypes.c_char_p
+    L.tpt_multi_upload_scene.argtypes = [P, ctypes.POINTER(SceneDesc)]
+    L.tpt_render_multi.argtypes = [P, ctypes.POINTER(RenderParams), P, P, ctypes.POINTER(Stats)]
     _lib = L
     return L
 
@@ -188,6 +198,54 @@ class Context:
     def close(self):
         if self.h:
             lib().tpt_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Multi:
+    """tpt_multi: one frame over several GPUs of this process (pixel shards + one RCCL
+    reduce onto the first device; Renderer.cpp:86-114 across devices)."""
+
+    def __init__(self, devices):
+        devs = np.ascontiguousarray(devices, np.int32)
+        h = ctypes.c_void_p()
+        rc = lib().tpt_multi_create(len(devs), _ptr(devs), ctypes.byref(h))
+        if rc != TPT_OK:
+            raise TptError("tpt_multi_create(%s) failed: %d" % (list(devs), rc))
+        self.h = h
+        self.width = self.height = 0
+
+    def _check(self, rc, what):
+        if rc != TPT_OK:
+            raise TptError("%s failed (%d): %s" % (what, rc, lib().tpt_multi_last_error(self.h).decode()))
+
+    def upload(self, preset_or_desc):
+        desc = preset_or_desc.desc if isinstance(preset_or_desc, Preset) else preset_or_desc
+        self._check(lib().tpt_multi_upload_scene(self.h, desc), "tpt_multi_upload_scene")
+        self.width, self.height = desc.contents.width, desc.contents.height
+        self._keep = preset_or_desc
+
+    def render(self, spp, mode=MODE_PT):
+        n = self.width * self.height * 3
+        rgb = np.zeros(n, np.float32)
+        splat = np.zeros(n, np.float32) if mode == MODE_BDPT else None
+        p = RenderParams(spp, mode, 0, 1, 0, 0)
+        st = Stats()
+        self._check(lib().tpt_render_multi(self.h, ctypes.byref(p), _ptr(rgb), _ptr(splat), ctypes.byref(st)),
+                    "tpt_render_multi")
+        rgb = rgb.reshape(self.height, self.width, 3)
+        if splat is not None:
+            splat = splat.reshape(self.height, self.width, 3)
+        return rgb, splat, st
+
+    def close(self):
+        if self.h:
+            lib().tpt_multi_destroy(self.h)
             self.h = None
 
     def __del__(self):
