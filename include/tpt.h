@@ -156,8 +156,9 @@ int tpt_render_device(tpt_ctx* ctx, const tpt_render_params* params, float* rgb_
 
 /* Closest-hit queries through the device BVH (Scene::Intersect, Scene.cpp:21-35).
  * rays: n*6 floats {origin, direction}; out: n*8 floats
- * {hit, x.xyz, N.xyz, primitive ordinal} (ordinal = triangle index in the soup,
- * spheres after all triangles, in object order; -1 on miss). */
+ * {hit, x.xyz, N.xyz, primitive ordinal} (ordinal = position of the hit Triangle /
+ * Sphere in the scene's object order: each mesh's triangles in file order, a sphere
+ * at its Scene::Add position; -1 on miss). */
 int tpt_intersect(tpt_ctx* ctx, const float* rays, int64_t n, int32_t cull, float* out);
 
 /* Camera scale (SceneRenderingHelper.cpp:12-14), computed on the host. */

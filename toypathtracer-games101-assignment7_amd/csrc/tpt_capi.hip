@@ -1104,6 +1104,25 @@ int tpt_intersect(tpt_ctx* c, const float* rays, int64_t n, int32_t cull, float*
             hipMemcpy(out, dout, n * 8 * sizeof(float), hipMemcpyDeviceToHost) != hipSuccess)
             rc = TPT_E_DEVICE;
     }
+    if (!rc) {
+        // primitive id (triangles first, then spheres) -> the scene's object-order
+        // ordinal: each mesh's triangles in file order, a sphere in its Add position
+        std::vector<int> ord(c->hs.tris.size() + c->hs.sph.size());
+        int next = 0;
+        for (size_t o = 0; o < c->hs.objs.size(); ++o) {
+            const DObj& ob = c->hs.objs[o];
+            if (ob.kind == TPT_OBJ_SPHERE) {
+                ord[ob.sphere_prim] = next++;
+            } else {
+                for (size_t t = 0; t < c->hs.tri_object.size(); ++t)
+                    if (c->hs.tri_object[t] == (int)o) ord[t] = next++;
+            }
+        }
+        for (int64_t k = 0; k < n; ++k) {
+            const int prim = (int)out[8 * k + 7];
+            if (prim >= 0 && prim < (int)ord.size()) out[8 * k + 7] = (float)ord[prim];
+        }
+    }
     (void)hipFree(dr);
     (void)hipFree(dout);
     if (rc) c->err = "intersect kernel failed";
