@@ -162,13 +162,16 @@ def cpu_baseline(key, scene, mode, threads, info):
     return out
 
 
-def valu_roofline(key, kernel_ms, shard_frac):
-    """VALU-issue roofline of the workload's dominant kernel (see module docstring)."""
+def valu_roofline(key, kernel_ms, samples):
+    """VALU-issue roofline of the workload's dominant kernel (see module docstring).
+    `samples`: pixel-samples this rank's launch traced; the profiled issue cycles are
+    per-sample constants of the workload, scaled to it."""
     model = _load_json("valu_model.json").get(key)
     if not model:
         return {"bound": "valu", "achieved": None, "peak": None, "unit": "G SIMD-cycles/s", "frac": None,
                 "traffic": None, "note": "profiles/valu_model.json has no entry for %s" % key}
-    cyc = model["issue_cycles_per_launch"] * shard_frac  # this rank's share of the frame
+    shard_frac = samples / float(model["samples_per_launch"])
+    cyc = model["issue_cycles_per_launch"] * shard_frac  # this rank's share of the profiled frame
     ms = kernel_ms
     achieved = cyc / (ms / 1e3) / 1e9
     clk = model.get("clock_mhz") or MAX_CLOCK_MHZ
@@ -284,7 +287,7 @@ class Runner:
                            "scene": scene, "mode": mode, "spp": spp, "width": W, "height": H,
                            "parallelism": "pixel-shard x%d + RCCL reduce" % self.world if self.world > 1
                            else "1 GPU"},
-                "roofline": valu_roofline(tkey, kernel_ms, shard_samples / float(W * H * spp)),
+                "roofline": valu_roofline(tkey, kernel_ms, shard_samples),
                 "roofline_hbm_model": hbm_model(scene, mode, kernel_ms, shard_samples, tkey),
                 "kernel_ms_per_step": round(kernel_ms, 3), "samples_per_rank_step": shard_samples}
         return line

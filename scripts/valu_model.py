@@ -95,6 +95,8 @@ def main():
     ap.add_argument("--frames", type=float, default=1.0)
     ap.add_argument("--scale", type=float, default=1.0)
     ap.add_argument("--waves", type=int, default=8, help="valu_cost column (8: issue-saturated)")
+    ap.add_argument("--samples", type=int, required=True,
+                    help="pixel-samples of the launch the figures are scaled to (784*784*spp)")
     ap.add_argument("--note", default="")
     ap.add_argument("--source", default=None, help="committed summary the figures come from (profiles/...)")
     a = ap.parse_args()
@@ -117,7 +119,7 @@ def main():
         per[name] = {"issue_cycles_per_launch": round(kcyc * f), "valu_insts_per_launch": round(kc.get("SQ_INSTS_VALU", 0) * f),
                      "kernel_ms_per_launch_kt": round(per_kt.get(name, 0) * 1e-6 * f, 3)}
     busy = cnt.get("SQ_BUSY_CYCLES")
-    entry = {"kernel": a.kernel, "issue_cycles_per_launch": round(cyc * f),
+    entry = {"kernel": a.kernel, "issue_cycles_per_launch": round(cyc * f), "samples_per_launch": a.samples,
              "valu_insts_per_launch": round(cnt.get("SQ_INSTS_VALU", 0) * f),
              "class_insts_per_launch": {k: round(v * f) for k, v in classes.items()},
              "other_insts_per_launch": round(other * f),

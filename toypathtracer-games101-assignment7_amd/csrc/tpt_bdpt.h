@@ -19,10 +19,8 @@
 //    either 1 or .8, so both variants are precomputed per vertex (`q1`, `q8`): the
 //    O(n^3) chain then costs a select and a multiply per step, same float ops in the
 //    same order.
-//  * Rays are traced as wave packets (tpt_device.h: traverse_packet /
-//    shadow_pts_packet).
-//  * The camera vertex v1 is the same for every sample (no jitter) and is hoisted
-//    out of the spp loop.
+//  * The camera vertices v0, v1 are the same for every sample (no jitter) and are
+//    computed once per pixel.
 //  * t = 1 splats (DrawToImage, SceneRenderingHelper.cpp:30-55) are fp32 atomics;
 //    zero contributions are skipped (adding +-0 never changes an fp32 sum here).
 #pragma once
@@ -119,71 +117,16 @@ TPT_D bool shadow_query(const DScene& s, const BVert& v1, const BVert& v2, int& 
     if (v2.prim >= 0 && dot3(-atob, v2.N) < 0.0f) return false;  // Scene.cpp:75-78
     return true;
 }
-template <bool kPacket>
-TPT_D bool shadow_v(const DScene& s, const BVert& v1, const BVert& v2, Packet pk, int* stk) {
+TPT_D bool shadow_v(const DScene& s, const BVert& v1, const BVert& v2) {
     int cull;
-    const bool test = shadow_query(s, v1, v2, cull);
-    bool sh = false;
-#ifndef TPT_LANE_SHADOW
-#define TPT_LANE_SHADOW 0  // per-lane shadow walk: 0 binary tree, 1 4-wide tree, 2 wave packet on the 4-wide tree
-#endif
-    if (test) {
-        if (kPacket || TPT_LANE_SHADOW == 2) sh = shadow_q_packet(s, v1.x, v2.x, cull, pk);
-        else if (TPT_LANE_SHADOW == 1) sh = shadow_q(s, v1.x, v2.x, cull, stk);
-        else sh = shadow_pts(s, v1.x, v2.x, cull, stk);
-    }
-    return sh;
-}
-
-// FillPathUsingRussianRoulette (BDPT.cpp:92-118) + SampleNextVertex (:261-279).
-template <bool kPacket>
-TPT_D int fill_path(const DScene& s, BVert* P, int start, uint32_t& rs, Packet pk, int* stk) {
-    int count = start + 1;
-    for (int i = start; i < kMaxLen - 1; i++) {
-        BVert cur = P[i];
-        if (cur.type == T_BG) break;
-        V3 wo = normalized(P[i - 1].x - cur.x);
-        const Mat m = load_mat(s, cur.mat);
-        float raw;
-        V3 wi = mat_sample(m, wo, cur.N, &raw, rs);
-        const float rr = i > 4 ? .8f : 1.f;
-        if (rng_float(rs) > rr) break;
-        float ct = (float)dabs_(dot3(cur.N, wi));
-        float sr = safe_div(raw, ct);
-        const Ray nr = make_ray(cur.x, wi);
-        const int cl = dot3(cur.N, wi) > 0.0f ? TPT_CULL_BACK : TPT_CULL_FRONT;
-        PTV it = kPacket ? scene_intersect_packet(s, nr, cl, pk) : scene_intersect(s, nr, cl, stk);
-        float pdf = srpdf_to_area(sr, cur.type, cur.x, cur.N, it.type, it.x, it.N);
-        if (pdf == 0.0f) break;
-        V3 bsdf = eval_bsdf(m, wo, wi, cur.N, false);
-        BVert nx;
-        nx.x = it.x; nx.N = it.N; nx.type = it.type; nx.prim = it.prim;
-        nx.mat = it.prim >= 0 ? prim_mat(s, it.prim) : -1;
-        nx.pdf = pdf * rr;
-        nx.alpha = divs(cur.alpha * safe_div(bsdf, sr), rr);
-        nx.q1 = nx.q8 = 0.0f;
-        P[i + 1] = nx;
-        count++;
-    }
-    return count;
-}
-
-// Reverse pdfs of vertices j = 0..count-3 (Append with last = j+1, Pre = j+2),
-// folded into the two possible cur_pdf factors safe_div(rev * rr, pdf_j).
-TPT_D void path_rev(const DScene& s, BVert* P, int count) {
-    for (int j = 0; j + 2 < count; ++j) {
-        const BVert& a = P[j + 1];
-        const float rev = append_pdf(s, a.type, a.mat, a.x, a.N, P[j + 2].x, P[j].type, P[j].x, P[j].N);
-        P[j].q1 = safe_div(rev * 1.f, P[j].pdf);
-        P[j].q8 = safe_div(rev * .8f, P[j].pdf);
-    }
+    return shadow_query(s, v1, v2, cull) && shadow_ray(s, v1.x, v2.x, cull);
 }
 
 // BDPTPath::PathWeight (BDPT.cpp:173-259) for light sub-length sl, camera sub-length tl.
 // Paths are read through an accessor P: P::cam(j), P::lit(j) return vertex records,
 // P::camq / P::litq the cached MIS factors (rr .8 when `r8`).
-template <class P, bool kPacket>
-TPT_D V3 path_weight(const DScene& s, const P& paths, int sl, int tl, Packet pk, int* stk TPT_STAMPS_ARG) {
+template <class P>
+TPT_D V3 path_weight(const DScene& s, const P& paths, int sl, int tl) {
     const int z = tl - 1;
     const BVert cz = paths.cam(z);
     if (cz.type == T_BG) return sl == 0 ? cz.alpha * v3(s.bg[0], s.bg[1], s.bg[2]) : v3s(0.0f);
@@ -191,7 +134,6 @@ TPT_D V3 path_weight(const DScene& s, const P& paths, int sl, int tl, Packet pk,
     if (sl != 0 && ly.type == T_BG) return v3s(0.0f);
     const V3 cpre = z >= 1 ? paths.cam(z - 1).x : cz.x;
     const V3 lpre = sl >= 2 ? paths.lit(sl - 2).x : ly.x;
-    TPT_STAMP(st, 1);
     V3 cst;
     float srA0 = 0.0f, srB0 = 0.0f;  // set when sl >= 1
     if (sl == 0) {
@@ -214,7 +156,6 @@ TPT_D V3 path_weight(const DScene& s, const P& paths, int sl, int tl, Packet pk,
         eval_pair_sa(s, cz.type, cz.mat, cz.x, cz.N, cpre, -dir, fc, srA0);
         cst = mul(fl * fc, (float)dabs_(dot3(normal_of(ly.type, ly.N), dir) * dot3(normal_of(cz.type, cz.N), -dir) / (double)d2));
     }
-    TPT_STAMP(st, 3);
     float wd = 1.0f;
     // loop A: camera prefix C[0..tl), append L[sl-1], ..., L[0]
     float cur = 1.0f;
@@ -233,7 +174,6 @@ TPT_D V3 path_weight(const DScene& s, const P& paths, int sl, int tl, Packet pk,
         wd += cur * cur;
         if (cur == 0.0f) break;
     }
-    TPT_STAMP(st, 4);
     // loop B: light prefix L[0..sl), append C[tl-1], ..., C[0]
     cur = 1.0f;
     for (int k = 0; k < tl; ++k) {
@@ -261,7 +201,6 @@ TPT_D V3 path_weight(const DScene& s, const P& paths, int sl, int tl, Packet pk,
         wd += cur * cur;
         if (cur == 0.0f) break;
     }
-    TPT_STAMP(st, 5);
     V3 lt = sl == 0 ? v3s(1.0f) : ly.alpha;
     V3 uc = lt * cz.alpha * cst;
     const V3 res = divs(uc, wd);
@@ -271,53 +210,18 @@ TPT_D V3 path_weight(const DScene& s, const P& paths, int sl, int tl, Packet pk,
         // skip zeros, so returning +0 without the test is exact.
         const V3 c = vmax0(res);
         if (c.x == 0.0f && c.y == 0.0f && c.z == 0.0f) return v3s(0.0f);
-        const bool shadowed = shadow_v<kPacket>(s, cz, ly, pk, stk);
-        if (s.dbg & 64) {
-            const unsigned long long act = __ballot(1), sh = __ballot(shadowed);
-            if (lane_id() == __builtin_ctzll(act)) {
-                atomicAdd(s.dbgc + 4, (unsigned long long)__popcll(act));
-                atomicAdd(s.dbgc + 5, (unsigned long long)__popcll(sh));
-            }
-        }
-        TPT_STAMP(st, 2);
-        if (shadowed) return v3s(0.0f);
+        if (shadow_v(s, cz, ly)) return v3s(0.0f);
     }
     return res;
 }
 
-// DrawToImage (SceneRenderingHelper.cpp:24-55), BlendMode::Additive, fp32 atomics.
-TPT_D void splat_add(const DScene& s, V3 light, V3 cam, V3 value, float* splat) {
-    if (value.x == 0.0f && value.y == 0.0f && value.z == 0.0f) return;
-    V3 d = normalized(light - cam);
-    d = divs(d, d.z);
-    float aspect = (float)(s.width / s.height);
-    V3 t = v3(-d.x / s.scale / aspect, -d.y / s.scale, 0.0f);
-    V3 uv = mul(t + v3s(1.0f), 0.5f);
-    float cx = uv.x * s.width, cy = uv.y * s.height;
-    int ix0 = (int)cx, iy0 = (int)cy;
-    for (int ix = ix0 - 1; ix <= ix0 + 1; ix++)
-        for (int iy = iy0 - 1; iy <= iy0 + 1; iy++) {
-            if (ix < 0 || iy < 0 || ix >= s.width || iy >= s.height) continue;
-            float dx = fabs_(cx - (ix + 0.5f)), dy = fabs_(cy - (iy + 0.5f));
-            float w = smax(0.0f, 1.0f - dx) * smax(0.0f, 1.0f - dy);
-            V3 c = mul(value, w);
-            float* b = splat + 3 * ((int64_t)ix + (int64_t)s.height * iy);
-            if (s.dbg & (256 | 512)) {  // profiling: 256 skips the atomics, 512 counts them
-                if (s.dbg & 512) atomicAdd(s.dbgc + 6, (unsigned long long)((c.x != 0.0f) + (c.y != 0.0f) + (c.z != 0.0f)));
-                continue;
-            }
-            if (c.x != 0.0f) atomicAdd(b + 0, c.x);
-            if (c.y != 0.0f) atomicAdd(b + 1, c.y);
-            if (c.z != 0.0f) atomicAdd(b + 2, c.z);
-        }
-}
-
-// DrawToImage for the splats of a whole wave (call with every lane of the wave that
-// is still in the loop; `want` marks the lanes that have a splat).  Same float ops
-// per tap as splat_add, but the adds are regrouped: a splat touches a 3x3 block of
+// DrawToImage (SceneRenderingHelper.cpp:24-55), BlendMode::Additive, fp32 atomics,
+// for the splats of a whole wave (call with every lane of the wave that is still in
+// the loop; `want` marks the lanes that have a splat).  Same float ops per tap as
+// the reference (zero contributions skipped), but the adds are regrouped: a splat touches a 3x3 block of
 // pixels = three row segments of 9 contiguous floats (rgb), so 27 lanes add one
 // splat with ONE atomic wave-instruction (two splats per instruction: lanes 0-26
-// and 32-58).  splat_add's per-lane form issues 64 adds to 64 scattered rows per
+// and 32-58).  A per-lane form issues 64 adds to 64 scattered rows per
 // instruction, which the memory-side atomic unit serves ~17x slower per byte
 // (MI355X_MICROARCH.md, Global float atomics).  Only the summation order changes,
 // and fp32 atomics have no fixed order anyway.
@@ -362,105 +266,19 @@ TPT_D void splat_wave(const DScene& s, bool want, V3 light, V3 cam, V3 value, fl
     }
 }
 
-struct PrivPaths {  // paths held in the lane's private arrays
-    const BVert* L;
-    const BVert* C;
-    TPT_D BVert cam(int j) const { return C[j]; }
-    TPT_D BVert lit(int j) const { return L[j]; }
-    TPT_D float camq(int j, bool r8) const { return r8 ? C[j].q8 : C[j].q1; }
-    TPT_D float litq(int j, bool r8) const { return r8 ? L[j].q8 : L[j].q1; }
-};
-
 // GenerateCameraPath's v0/v1 (BDPT.cpp:41-59): identical for every sample of a pixel.
-TPT_D void camera_vertices(const DScene& s, int64_t i, BVert& c0, BVert& c1, int* stk) {
+TPT_D void camera_vertices(const DScene& s, int64_t i, BVert& c0, BVert& c1) {
     const int px = (int)(i % s.width), py = (int)(i / s.width);
     const V3 dir = pixel_ray(px, py, s.width, s.height, s.scale);
     const V3 eye = v3(s.eye[0], s.eye[1], s.eye[2]);
     c0.x = eye; c0.N = v3s(0.0f); c0.type = T_CAM; c0.prim = -1; c0.mat = -1;
     c0.pdf = kCamZeroPdf; c0.alpha = v3s(1.0f); c0.q1 = c0.q8 = 0.0f;
-    PTV h1 = scene_intersect(s, make_ray(eye, dir), TPT_CULL_BACK, stk);
+    PTV h1 = scene_intersect(s, make_ray(eye, dir), TPT_CULL_BACK);
     c1.x = h1.x; c1.N = h1.N; c1.type = h1.type; c1.prim = h1.prim;
     c1.mat = h1.prim >= 0 ? prim_mat(s, h1.prim) : -1;
     c1.pdf = srpdf_to_area(kCamRayPdf, T_CAM, c0.x, c0.N, h1.type, h1.x, h1.N);
     c1.alpha = v3s(1.0f);
     c1.q1 = c1.q8 = 0.0f;
-}
-
-// One BDPT sample's subpaths (BDPT.cpp:286-287) and their cached MIS factors.
-template <bool kPacket>
-TPT_D void generate_paths(const DScene& s, const BVert& c0, const BVert& c1, uint32_t& rs, BVert* C, BVert* L,
-                          int& cn, int& ln, Packet pk, int* stk) {
-    C[0] = c0;
-    C[1] = c1;
-    cn = 2;
-    if (c1.type != T_BG) cn = fill_path<kPacket>(s, C, 1, rs, pk, stk);
-    // GenerateLightPath (BDPT.cpp:61-90) from m_emissionObjects[0]
-    const DObj lo = s.objs[s.emitters[0]];
-    const V3 lem = load_mat(s, lo.mat).em;
-    V3 pc, pn;
-    int pp;
-    object_sample(s, lo, pc, pn, pp, rs);
-    BVert l0;
-    l0.x = pc; l0.N = pn; l0.type = T_LIGHT; l0.prim = pp; l0.mat = lo.mat;
-    l0.pdf = lo.pdf;
-    l0.alpha = divs(lem, l0.pdf);
-    l0.q1 = l0.q8 = 0.0f;
-    float pdf1;
-    V3 wi = cosine_sample(pn, pdf1, rs);
-    float ct = (float)dot3(l0.N, wi);
-    pdf1 = safe_div(pdf1, ct);
-    const Ray lr = make_ray(l0.x, wi);
-    PTV it = kPacket ? scene_intersect_packet(s, lr, TPT_CULL_BACK, pk) : scene_intersect(s, lr, TPT_CULL_BACK, stk);
-    BVert l1;
-    l1.x = it.x; l1.N = it.N; l1.type = it.type; l1.prim = it.prim;
-    l1.mat = it.prim >= 0 ? prim_mat(s, it.prim) : -1;
-    l1.pdf = srpdf_to_area(pdf1, T_LIGHT, l0.x, l0.N, it.type, it.x, it.N);
-    l1.alpha = v3s(0.0f);  // fresh InternalPathVertex (BDPT.hpp:19)
-    l1.q1 = l1.q8 = 0.0f;
-    L[0] = l0;
-    if (pdf1 != 0.0f) l1.alpha = safe_div(l0.alpha, pdf1);
-    L[1] = l1;
-    if (pdf1 == 0.0f && it.type == T_BG) ln = 2;
-    else ln = fill_path<kPacket>(s, L, 1, rs, pk, stk);
-    path_rev(s, C, cn);
-    path_rev(s, L, ln);
-}
-
-// One pixel stream, all strategies in one lane (Renderer.cpp:42-52 with BDPT,
-// BDPT.cpp:282-315).  Used for short pixel lists; full frames use the wavefront
-// kernels (tpt_capi.hip), which balance strategies across lanes.
-template <bool kPacket>
-TPT_D void bdpt_pixel(const DScene& s, int64_t i, int spp, V3& acc, float* splat, unsigned long long& nbounce,
-                      Packet pk, int* stk) {
-    BVert C[kMaxLen], L[kMaxLen];
-    BVert c0, c1;
-    camera_vertices(s, i, c0, c1, stk);
-    const float inv = 1.0f / spp;
-    uint32_t rs = (uint32_t)((int)i + 1);
-    acc = v3s(0.0f);
-    PrivPaths paths;
-    paths.L = L;
-    paths.C = C;
-    for (int sp = 0; sp < spp; ++sp) {
-        int cn, ln;
-        generate_paths<kPacket>(s, c0, c1, rs, C, L, cn, ln, pk, stk);
-        nbounce += (unsigned long long)(cn + ln);
-        V3 res = v3s(0.0f);
-        // (t, s) strategies in the reference's order (t outer, s inner); pi = 0 is
-        // (t=1, s=0): t + s < 2, skipped.
-        const int np = cn * (ln + 1);
-        for (int pi = 1; pi < np; ++pi) {
-            const int t = pi / (ln + 1) + 1, sl = pi % (ln + 1);
-#ifdef TPT_STAMPS
-            Stamps st{};
-            st.last = stamp_now();
-#endif
-            V3 w = vmax0(path_weight<PrivPaths, kPacket>(s, paths, sl, t, pk, stk TPT_STAMPS_PASS));
-            if (t > 1) res = res + w;
-            else if (splat) splat_add(s, L[sl - 1].x, C[0].x, w, splat);
-        }
-        acc = acc + mul(res, inv);
-    }
 }
 
 // ------------------------------------------------------------ wavefront --
@@ -512,89 +330,18 @@ TPT_D void rec_store_q(const WfState& w, int slot, int64_t k, float q1, float q8
     *reinterpret_cast<float2*>(rec_at(w.rec, k, slot) + 3) = make_float2(q1, q8);
 }
 
-// fill_path + path_rev streamed into the HBM records, one vertex per call: the
-// body of FillPathUsingRussianRoulette's loop (BDPT.cpp:92-118) for the subpath at
-// slots base.. whose last two vertices are prev = P[i-1] and cur = P[i].  Same
-// vertices, draws and float ops as fill_path + path_rev; vertex j's reverse pdf
-// needs P[j], P[j+1] and P[j+2].x, so it is computed as soon as P[j+2] exists and
-// only a three-vertex window is live.  Returns false when the subpath has ended
-// (its vertex count is then i + 1).
-template <bool kPacket>
-TPT_D bool extend_rec(const DScene& s, const WfState& w, int64_t k, int base, BVert& prev, BVert& cur, int& i,
-                      uint32_t& rs, Packet pk, int* stk) {
-    if (i >= kMaxLen - 1 || cur.type == T_BG) return false;
-    V3 wo = normalized(prev.x - cur.x);
-    const Mat m = load_mat(s, cur.mat);
-    float raw;
-    V3 wi = mat_sample(m, wo, cur.N, &raw, rs);
-    const float rr = i > 4 ? .8f : 1.f;
-    if (rng_float(rs) > rr) return false;
-    float ct = (float)dabs_(dot3(cur.N, wi));
-    float sr = safe_div(raw, ct);
-    const Ray nr = make_ray(cur.x, wi);
-    const int cl = dot3(cur.N, wi) > 0.0f ? TPT_CULL_BACK : TPT_CULL_FRONT;
-    PTV it = kPacket ? scene_intersect_packet(s, nr, cl, pk) : scene_intersect(s, nr, cl, stk);
-    float pdf = srpdf_to_area(sr, cur.type, cur.x, cur.N, it.type, it.x, it.N);
-    if (pdf == 0.0f) return false;
-    V3 bsdf = eval_bsdf(m, wo, wi, cur.N, false);
-    BVert nx;
-    nx.x = it.x; nx.N = it.N; nx.type = it.type; nx.prim = it.prim;
-    nx.mat = it.prim >= 0 ? prim_mat(s, it.prim) : -1;
-    nx.pdf = pdf * rr;
-    nx.alpha = divs(cur.alpha * safe_div(bsdf, sr), rr);
-    nx.q1 = nx.q8 = 0.0f;
-    rec_store(w, base + i + 1, k, nx);
-    // path_rev for j = i - 1: Append(P[j]) after last = P[i], Pre = P[i+1]
-    const float rev = append_pdf(s, cur.type, cur.mat, cur.x, cur.N, nx.x, prev.type, prev.x, prev.N);
-    rec_store_q(w, base + i - 1, k, safe_div(rev * 1.f, prev.pdf), safe_div(rev * .8f, prev.pdf));
-    prev = cur;
-    cur = nx;
-    ++i;
-    return true;
-}
-
-// GenerateLightPath's first two vertices (BDPT.cpp:61-90, m_emissionObjects[0]),
-// stored at slots kMaxLen, kMaxLen + 1.  Returns false when the path ends there
-// (pdf1 == 0 and the ray escaped: ln = 2).
-template <bool kPacket>
-TPT_D bool light_start_rec(const DScene& s, const WfState& w, int64_t k, BVert& l0, BVert& l1, uint32_t& rs,
-                           Packet pk, int* stk) {
-    const DObj lo = s.objs[s.emitters[0]];
-    V3 pc, pn;
-    int pp;
-    object_sample(s, lo, pc, pn, pp, rs);
-    l0.x = pc; l0.N = pn; l0.type = T_LIGHT; l0.prim = pp; l0.mat = lo.mat;
-    l0.pdf = lo.pdf;
-    l0.alpha = divs(load_mat(s, lo.mat).em, l0.pdf);
-    l0.q1 = l0.q8 = 0.0f;
-    float pdf1;
-    V3 wi = cosine_sample(pn, pdf1, rs);
-    float ct = (float)dot3(l0.N, wi);
-    pdf1 = safe_div(pdf1, ct);
-    const Ray lr = make_ray(l0.x, wi);
-    PTV it = kPacket ? scene_intersect_packet(s, lr, TPT_CULL_BACK, pk) : scene_intersect(s, lr, TPT_CULL_BACK, stk);
-    l1.x = it.x; l1.N = it.N; l1.type = it.type; l1.prim = it.prim;
-    l1.mat = it.prim >= 0 ? prim_mat(s, it.prim) : -1;
-    l1.pdf = srpdf_to_area(pdf1, T_LIGHT, l0.x, l0.N, it.type, it.x, it.N);
-    l1.alpha = v3s(0.0f);  // fresh InternalPathVertex (BDPT.hpp:19)
-    l1.q1 = l1.q8 = 0.0f;
-    if (pdf1 != 0.0f) l1.alpha = safe_div(l0.alpha, pdf1);
-    rec_store(w, kMaxLen, k, l0);
-    rec_store(w, kMaxLen + 1, k, l1);
-    return !(pdf1 == 0.0f && it.type == T_BG);
-}
-
 // One generation step of a lane's sample, for the persistent gen kernel: either
-// GenerateLightPath's start (phase 1: light vertex l0 and the first bounce l1,
-// BDPT.cpp:61-90) or one iteration of FillPathUsingRussianRoulette's loop
-// (extend_rec).  Both end in ONE closest-hit query, so a wave whose lanes are in
-// different phases traces a single query instead of one per phase (the light start
-// used to run beside every extension step).  Same draws, vertices and float ops as
-// light_start_rec / extend_rec.  Returns false when the current subpath has ended:
-// its vertex count is then i + 1.
-template <bool kPacket>
+// GenerateLightPath's start (phase 1: light vertex l0 from m_emissionObjects[0] and
+// the first bounce l1, BDPT.cpp:61-90) or one iteration of
+// FillPathUsingRussianRoulette's loop (BDPT.cpp:92-118 with SampleNextVertex,
+// :261-279).  Both end in ONE closest-hit query, so a wave whose lanes are in
+// different phases traces a single query.  Vertices stream into the HBM records as
+// they are made; vertex j's reverse pdf (Append(P[j]) after last = P[j+1], Pre =
+// P[j+2], folded into q1 / q8) is written as soon as P[j+2] exists, so only a
+// three-vertex window is live.  Same draws, vertices and float ops as the reference.
+// Returns false when the current subpath has ended: its vertex count is then i + 1.
 TPT_D bool gen_step(const DScene& s, const WfState& w, int64_t k, int& phase, BVert& prev, BVert& cur, int& i,
-                    uint32_t& rs, Packet pk, int* stk) {
+                    uint32_t& rs) {
     const bool start = phase == 1;
     bool go = true;
     Ray ray;
@@ -634,7 +381,7 @@ TPT_D bool gen_step(const DScene& s, const WfState& w, int64_t k, int& phase, BV
         }
     }
     if (!go) return false;
-    PTV it = kPacket ? scene_intersect_packet(s, ray, cl, pk) : scene_intersect(s, ray, cl, stk);
+    PTV it = scene_intersect(s, ray, cl);
     const float pdf = srpdf_to_area(sr, cur.type, cur.x, cur.N, it.type, it.x, it.N);
     BVert nx;
     nx.x = it.x; nx.N = it.N; nx.type = it.type; nx.prim = it.prim;

@@ -27,64 +27,50 @@ using namespace tpt;
 // ------------------------------------------------------------------ kernels --
 extern __shared__ __align__(16) unsigned char tpt_smem[];
 
-// Per-wave packet stacks (4 waves per workgroup).
-#define TPT_PACKET_DECL                                                   \
-    __shared__ int pk_node[kBlock / 64][kStackCap];                       \
-    __shared__ unsigned long long pk_mask[kBlock / 64][kStackCap];        \
-    Packet pk;                                                            \
-    pk.node = pk_node[threadIdx.x / 64];                                  \
-    pk.mask = pk_mask[threadIdx.x / 64];
-
-// Workgroup prologue: LDS = [traversal stack: max_stack x kBlock ints][tnodes][tris][qnodes][mats].
-// With kLds the scene's node and triangle arrays are copied into LDS (16 B per lane
-// per step) and the kernel's DScene is pointed at them, so every traversal fetch is
-// a ds_read instead of a dependent L1/L2 load.
+// Workgroup prologue: LDS = [tnodes][tris][mats][leaves][groups][ftris].  With kLds
+// the scene's node and triangle arrays are copied into LDS (16 B per lane per step)
+// and the kernel's DScene is pointed at them, so every traversal fetch is a ds_read
+// instead of a dependent L1/L2 load.  Returns the first LDS byte after the scene.
 template <bool kLds>
-TPT_D int* stage_scene(DScene& s) {
-    int* stk = reinterpret_cast<int*>(tpt_smem) + threadIdx.x;
-    if (kLds) {
-        unsigned char* base = tpt_smem + (size_t)s.max_stack * kBlock * sizeof(int);
-        const bool full = s.lds_full != 0;  // else only the flat-query arrays (+ ftris at the end)
-        const int nb = full ? s.nnodes * (int)sizeof(DNode) : 0, tb = full ? s.ntri * (int)sizeof(DTri) : 0,
-                  qb = full ? s.nqnodes * (int)sizeof(DQNode) : 0, mb = s.nmats * (int)sizeof(DMat);
-        const uint4* gn = reinterpret_cast<const uint4*>(s.tnodes);
-        const uint4* gt = reinterpret_cast<const uint4*>(s.tris);
-        const uint4* gq = reinterpret_cast<const uint4*>(s.qnodes);
-        uint4* ln = reinterpret_cast<uint4*>(base);
-        uint4* lt = reinterpret_cast<uint4*>(base + nb);
-        uint4* lq = reinterpret_cast<uint4*>(base + nb + tb);
-        for (int i = threadIdx.x; i < nb / 16; i += kBlock) ln[i] = gn[i];
-        for (int i = threadIdx.x; i < tb / 16; i += kBlock) lt[i] = gt[i];
-        for (int i = threadIdx.x; i < qb / 16; i += kBlock) lq[i] = gq[i];
-        const uint4* gm = reinterpret_cast<const uint4*>(s.mats);
-        uint4* lm = reinterpret_cast<uint4*>(base + nb + tb + qb);
-        for (int i = threadIdx.x; i < (mb + 15) / 16; i += kBlock) lm[i] = gm[i];  // 72-B records: round up
-        const int lo = nb + tb + qb + ((mb + 15) & ~15), lb = s.nleaf * (int)sizeof(DNode);
-        const uint4* gl = reinterpret_cast<const uint4*>(s.leaves);
-        uint4* ll = reinterpret_cast<uint4*>(base + lo);
-        for (int i = threadIdx.x; i < lb / 16; i += kBlock) ll[i] = gl[i];
-        const int go = lo + lb, gb = s.ngroup * (int)sizeof(DNode);
-        const uint4* gg = reinterpret_cast<const uint4*>(s.groups);
-        uint4* lg = reinterpret_cast<uint4*>(base + go);
-        for (int i = threadIdx.x; i < gb / 16; i += kBlock) lg[i] = gg[i];
-        const int fo = go + gb, fb = full ? 0 : s.nleaf * (int)sizeof(DTri);
-        const uint4* gf = reinterpret_cast<const uint4*>(s.ftris);
-        uint4* lf = reinterpret_cast<uint4*>(base + fo);
-        for (int i = threadIdx.x; i < fb / 16; i += kBlock) lf[i] = gf[i];
-        __syncthreads();
-        s.leaves = reinterpret_cast<const DNode*>(base + lo);
-        s.groups = reinterpret_cast<const DNode*>(base + go);
-        s.mats = reinterpret_cast<const DMat*>(base + nb + tb + qb);
-        if (full) {
-            s.tnodes = reinterpret_cast<const DNode*>(base);  // the binary `nodes` stay in L1/L2 (light sampling)
-            s.tris = reinterpret_cast<const DTri*>(base + nb);
-            s.qnodes = reinterpret_cast<const DQNode*>(base + nb + tb);
-            s.ftris = s.tris;
-        } else {
-            s.ftris = reinterpret_cast<const DTri*>(base + fo);
-        }
+TPT_D unsigned char* stage_scene(DScene& s) {
+    if (!kLds) return tpt_smem;
+    unsigned char* base = tpt_smem;
+    const bool full = s.lds_full != 0;  // else only the flat-query arrays (+ ftris at the end)
+    const int nb = full ? s.nnodes * (int)sizeof(DNode) : 0, tb = full ? s.ntri * (int)sizeof(DTri) : 0,
+              mb = s.nmats * (int)sizeof(DMat);
+    const uint4* gn = reinterpret_cast<const uint4*>(s.tnodes);
+    const uint4* gt = reinterpret_cast<const uint4*>(s.tris);
+    uint4* ln = reinterpret_cast<uint4*>(base);
+    uint4* lt = reinterpret_cast<uint4*>(base + nb);
+    for (int i = threadIdx.x; i < nb / 16; i += kBlock) ln[i] = gn[i];
+    for (int i = threadIdx.x; i < tb / 16; i += kBlock) lt[i] = gt[i];
+    const uint4* gm = reinterpret_cast<const uint4*>(s.mats);
+    uint4* lm = reinterpret_cast<uint4*>(base + nb + tb);
+    for (int i = threadIdx.x; i < (mb + 15) / 16; i += kBlock) lm[i] = gm[i];  // 72-B records: round up
+    const int lo = nb + tb + ((mb + 15) & ~15), lb = s.nleaf * (int)sizeof(DNode);
+    const uint4* gl = reinterpret_cast<const uint4*>(s.leaves);
+    uint4* ll = reinterpret_cast<uint4*>(base + lo);
+    for (int i = threadIdx.x; i < lb / 16; i += kBlock) ll[i] = gl[i];
+    const int go = lo + lb, gb = s.ngroup * (int)sizeof(DNode);
+    const uint4* gg = reinterpret_cast<const uint4*>(s.groups);
+    uint4* lg = reinterpret_cast<uint4*>(base + go);
+    for (int i = threadIdx.x; i < gb / 16; i += kBlock) lg[i] = gg[i];
+    const int fo = go + gb, fb = full ? 0 : s.nleaf * (int)sizeof(DTri);
+    const uint4* gf = reinterpret_cast<const uint4*>(s.ftris);
+    uint4* lf = reinterpret_cast<uint4*>(base + fo);
+    for (int i = threadIdx.x; i < fb / 16; i += kBlock) lf[i] = gf[i];
+    __syncthreads();
+    s.leaves = reinterpret_cast<const DNode*>(base + lo);
+    s.groups = reinterpret_cast<const DNode*>(base + go);
+    s.mats = reinterpret_cast<const DMat*>(base + nb + tb);
+    if (full) {
+        s.tnodes = reinterpret_cast<const DNode*>(base);  // the binary `nodes` stay in L1/L2 (light sampling)
+        s.tris = reinterpret_cast<const DTri*>(base + nb);
+        s.ftris = s.tris;
+    } else {
+        s.ftris = reinterpret_cast<const DTri*>(base + fo);
     }
-    return stk;
+    return base + s.lds_bytes;
 }
 
 #ifndef TPT_PT_MINWAVES
@@ -124,8 +110,7 @@ __global__ __launch_bounds__(kBlock, TPT_PT_MINWAVES) void tpt_pt_kernel(DScene 
                                                                         int64_t stride, int64_t count,
                                                                         const int64_t* __restrict__ list,
                                                                         float* __restrict__ out, int Q) {
-    int* stk = stage_scene<kLds>(s);
-    TPT_PACKET_DECL
+    unsigned char* lds_free = stage_scene<kLds>(s);
     const int64_t gl = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     const int64_t k = gl / Q;      // pixel ordinal in the shard / list
     const int q = (int)(gl % Q);   // this lane's sample phase
@@ -135,30 +120,23 @@ __global__ __launch_bounds__(kBlock, TPT_PT_MINWAVES) void tpt_pt_kernel(DScene 
     const int px = (int)(i % s.width), py = (int)(i / s.width);
     const V3 dir = pixel_ray(px, py, s.width, s.height, s.scale);
     const Ray r = make_ray(v3(s.eye[0], s.eye[1], s.eye[2]), dir);
-    PTV v = scene_intersect(s, r, TPT_CULL_BACK, stk);
+    PTV v = scene_intersect(s, r, TPT_CULL_BACK);
     const bool hit = on && v.type != T_BG;
     V3 acc = v3s(0.0f);
     if (hit) {
         const int mi = prim_mat(s, v.prim);
         const Mat m = load_mat(s, mi);
         PixPark px;
-        px.base = reinterpret_cast<float*>(tpt_smem + (size_t)s.max_stack * kBlock * sizeof(int) +
-                                           (kLds ? (size_t)s.lds_bytes : 0));
+        px.base = reinterpret_cast<float*>(lds_free);
         px.park(v.x, v.N, -dir, mi, m);
         const float inv = 1.0f / spp;
         uint32_t rs = (uint32_t)((int)i + 1);  // ResetRandom(i + 1), Renderer.cpp:42
         rs = skip_samples(rs, m.type, s.light_draws, q);
         const int base = lane_id() - q;       // first lane of this pixel (Q divides 64)
-#ifdef TPT_STAMPS
-        Stamps st{};
-        st.last = stamp_now();
-#endif
         for (int j0 = 0; j0 < spp; j0 += Q) {
             V3 L = v3s(0.0f);
-            TPT_STAMP(st, 0);
             if (j0 + q < spp) {
-                L = mul(pt_sample(s, px, rs, stk, pk TPT_STAMPS_PASS), inv);
-                TPT_STAMP(st, 11);
+                L = mul(pt_sample(s, px, rs), inv);
                 if (Q > 1) rs = skip_samples(rs, m.type, s.light_draws, Q - 1);
             }
             if (Q == 1) {
@@ -172,11 +150,6 @@ __global__ __launch_bounds__(kBlock, TPT_PT_MINWAVES) void tpt_pt_kernel(DScene 
                 }
             }
         }
-#ifdef TPT_STAMPS
-        TPT_STAMP(st, 0);
-        if (lane_id() == 0)
-            for (int x = 0; x < 12; ++x) atomicAdd(s.dbgc + 8 + x, st.acc[x]);
-#endif
     }
     if (on && q == 0) {
         out[3 * row + 0] = acc.x;
@@ -207,8 +180,7 @@ __global__ __launch_bounds__(kBlock, TPT_PTI_MINWAVES) void tpt_pti_kernel(DScen
                                                                           const int64_t* __restrict__ list,
                                                                           float* __restrict__ out,
                                                                           unsigned long long* __restrict__ bounces) {
-    int* stk = stage_scene<kLds>(s);
-    TPT_PACKET_DECL
+    stage_scene<kLds>(s);
     const int64_t k = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     const bool on = k < count;
     const int64_t i = on ? (list ? list[k] : begin + k * stride) : 0;
@@ -227,8 +199,8 @@ __global__ __launch_bounds__(kBlock, TPT_PTI_MINWAVES) void tpt_pti_kernel(DScen
     for (int j = on ? 0 : spp; j < spp;) {
         bool live = !(p.alpha.x == 0.0f && p.alpha.y == 0.0f && p.alpha.z == 0.0f) && p.nb < kPtiMaxBounces;  // :54-55
         if (live) {
-            const PTV v = scene_intersect(s, p.r, p.flip ? TPT_CULL_FRONT : TPT_CULL_BACK, stk);  // :56
-            live = v.type != T_BG && pti_step(s, v, p, rs, stk, pk);                              // :58-131
+            const PTV v = scene_intersect(s, p.r, p.flip ? TPT_CULL_FRONT : TPT_CULL_BACK);  // :56
+            live = v.type != T_BG && pti_step(s, v, p, rs);                                   // :58-131
         }
         if (!live) {
             acc = acc + mul(p.res, inv);  // Renderer.cpp:49 `fb[i] += (1.0f / spp) * L`
@@ -251,33 +223,7 @@ __global__ __launch_bounds__(kBlock, TPT_PTI_MINWAVES) void tpt_pti_kernel(DScen
     if (lane_id() == 0) atomicAdd(bounces, nbt);
 }
 
-// BDPT: Renderer.cpp:38-52 + :58-60 for TPT_MODE_BDPT.  t=1 strategies splat into
-// `splat` with fp32 atomics (the reference sums per-thread buffers instead,
-// Renderer.cpp:98-114: same values, different summation order).
-template <bool kLds>
-__global__ __launch_bounds__(kBlock) void tpt_bdpt_kernel(DScene s, int spp, int64_t begin, int64_t stride,
-                                                          int64_t count, const int64_t* __restrict__ list,
-                                                          float* __restrict__ out, float* __restrict__ splat,
-                                                          unsigned long long* __restrict__ bounces) {
-    int* stk = stage_scene<kLds>(s);
-    TPT_PACKET_DECL
-    const int64_t k = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (k >= count) return;
-    const int64_t i = list ? list[k] : begin + k * stride;
-    const int64_t row = list ? k : i;
-    V3 acc = v3s(0.0f);
-    unsigned long long nb = 0;
-    bdpt_pixel<false>(s, i, spp, acc, splat, nb, pk, stk);
-    out[3 * row + 0] = acc.x;
-    out[3 * row + 1] = acc.y;
-    out[3 * row + 2] = acc.z;
-    if (bounces) atomicAdd(bounces, nb);
-}
-
 // ---- wavefront BDPT kernels (see tpt_bdpt.h, "wavefront") --------------------
-#ifndef TPT_GEN_PACKET
-#define TPT_GEN_PACKET false  // wave-packet closest hits in gen (A/B)
-#endif
 #ifndef TPT_GEN_MINWAVES
 #define TPT_GEN_MINWAVES 4  // waves per SIMD (measured: 4 beats 3 and 5)
 #endif
@@ -295,8 +241,7 @@ __global__ __launch_bounds__(kBlock) void tpt_bdpt_kernel(DScene s, int spp, int
 template <bool kLds>
 __global__ __launch_bounds__(kBlock, TPT_GEN_MINWAVES) void tpt_bdpt_gen_kernel(DScene s, WfState w, int iter,
                                                                                unsigned* __restrict__ queue) {
-    int* stk = stage_scene<kLds>(s);
-    TPT_PACKET_DECL
+    stage_scene<kLds>(s);
     const int shard = blockIdx.x & 7;
     const int64_t k_lo = w.n * shard / 8, k_hi = w.n * (shard + 1) / 8;
     unsigned* q = queue + shard * 16;  // 64 B apart
@@ -331,7 +276,7 @@ __global__ __launch_bounds__(kBlock, TPT_GEN_MINWAVES) void tpt_bdpt_gen_kernel(
                         c0 = P.cam(0);
                         c1 = P.cam(1);
                     } else {
-                        camera_vertices(s, pix, c0, c1, stk);
+                        camera_vertices(s, pix, c0, c1);
                         rec_store(w, 0, k, c0);
                         rec_store(w, 1, k, c1);
                     }
@@ -349,7 +294,7 @@ __global__ __launch_bounds__(kBlock, TPT_GEN_MINWAVES) void tpt_bdpt_gen_kernel(
         if (__ballot(k >= 0) == 0) break;  // every lane idle and its shard drained
         if (k < 0) continue;
         int ln = -1;  // >= 0: the pixel's sample is complete
-        if (!gen_step<TPT_GEN_PACKET>(s, w, k, phase, prev, cur, i, rs, pk, stk)) {
+        if (!gen_step(s, w, k, phase, prev, cur, i, rs)) {
             if (phase == 0) {
                 cn = i + 1;
                 phase = 1;
@@ -427,38 +372,21 @@ __global__ __launch_bounds__(kBlock) void tpt_bdpt_scatter_kernel(WfState w, uns
 // wave stays in the loop until the wave is done (splat_wave needs the whole wave).
 template <bool kLds>
 __global__ __launch_bounds__(kBlock, TPT_CONN_MINWAVES) void tpt_bdpt_conn_kernel(DScene s, WfState w, float* __restrict__ splat) {
-    int* stk = stage_scene<kLds>(s);
-    TPT_PACKET_DECL
+    stage_scene<kLds>(s);
     const int64_t total = total_tasks(w);
     const V3 eye = v3(s.eye[0], s.eye[1], s.eye[2]);
-#ifdef TPT_STAMPS
-    Stamps st{};
-    st.last = stamp_now();
-#endif
     for (int64_t g0 = (int64_t)blockIdx.x * kBlock + (threadIdx.x & ~63); g0 < total;
          g0 += (int64_t)gridDim.x * kBlock) {
         const int64_t g = g0 + lane_id();
         V3 v = v3s(0.0f), lx = eye;
         bool sp = false;
         if (g < total) {
-            TPT_STAMP(st, 0);
             const unsigned long long tk = w.task[g];
             const int64_t k = (int64_t)(tk & 0xffffffffffull);
             const int t = (int)((tk >> 40) & 0xff), sl = (int)(tk >> 48);
             GlobPaths P;
             P.rec = rec_at(w.rec, k, 0);
-            v = vmax0(path_weight<GlobPaths, false>(s, P, sl, t, pk, stk TPT_STAMPS_PASS));
-            TPT_STAMP(st, 6);
-            if (s.dbg & 64) {  // strategy census: all / s = 0 / zero result
-                const unsigned long long act = __ballot(1), z = __ballot(v.x == 0.0f && v.y == 0.0f && v.z == 0.0f),
-                                         e = __ballot(sl == 0);
-                if (lane_id() == __builtin_ctzll(act)) {
-                    atomicAdd(s.dbgc + 0, (unsigned long long)__popcll(act));
-                    atomicAdd(s.dbgc + 1, (unsigned long long)__popcll(e));
-                    atomicAdd(s.dbgc + 2, (unsigned long long)__popcll(z));
-                    atomicAdd(s.dbgc + 3, (unsigned long long)__popcll(z & ~e));
-                }
-            }
+            v = vmax0(path_weight(s, P, sl, t));
             if (t > 1) {
                 const int64_t ri = w.tres[g];
                 w.res[3 * ri] = v.x;
@@ -470,18 +398,12 @@ __global__ __launch_bounds__(kBlock, TPT_CONN_MINWAVES) void tpt_bdpt_conn_kerne
             }
         }
         // t = 1: DrawToImage of the light vertex (BDPT.cpp:303-305), whole wave
-        if (splat && !(s.dbg & 1024)) splat_wave(s, sp, lx, eye, v, splat);  // 1024: profiling ablation
-        TPT_STAMP(st, 7);
+        if (splat) splat_wave(s, sp, lx, eye, v, splat);
     }
-#ifdef TPT_STAMPS
-    TPT_STAMP(st, 0);
-    if (lane_id() == 0)
-        for (int x = 0; x < 12; ++x) atomicAdd(s.dbgc + 8 + x, st.acc[x]);
-#endif
 }
 
 #ifndef TPT_FLAT_DEFAULT
-#define TPT_FLAT_DEFAULT 7  // measured: BDPT 882 -> 812 ms, PT 64.0 -> 61.3 ms
+#define TPT_FLAT_DEFAULT 3  // kFlatShadow | kFlatHit; measured: BDPT 882 -> 812 ms, PT 64.0 -> 61.3 ms
 #endif
 __global__ __launch_bounds__(kBlock) void tpt_bdpt_fold_kernel(WfState w, float inv) {
     const int64_t k = (int64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -516,12 +438,11 @@ __global__ void tpt_scale_kernel(float* __restrict__ buf, int64_t n, float spp) 
 // Closest-hit queries (Scene::Intersect) for tpt_intersect.
 __global__ __launch_bounds__(kBlock) void tpt_intersect_kernel(DScene s, const float* __restrict__ rays, int64_t n,
                                                                int cull, float* __restrict__ out) {
-    int* stk = stage_scene<false>(s);
     const int64_t k = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (k >= n) return;
     const float* q = rays + 6 * k;
     Ray r = make_ray(v3(q[0], q[1], q[2]), v3(q[3], q[4], q[5]));
-    PTV v = scene_intersect(s, r, cull, stk);
+    PTV v = scene_intersect(s, r, cull);
     float* o = out + 8 * k;
     o[0] = v.type == T_BG ? 0.f : 1.f;
     o[1] = v.x.x; o[2] = v.x.y; o[3] = v.x.z;
@@ -530,6 +451,15 @@ __global__ __launch_bounds__(kBlock) void tpt_intersect_kernel(DScene s, const f
 }
 
 // ------------------------------------------------------------------ C ABI --
+#ifndef TPT_PT_LANES
+#define TPT_PT_LANES 8  // Q lanes per PT pixel stream (1, 2, 4, 8 or 16; 8 measured best on one MI355X)
+#endif
+#ifndef TPT_BDPT_SERIAL
+#define TPT_BDPT_SERIAL 0  // 1: connect / fold on the gen stream (per-kernel timing builds only)
+#endif
+static_assert(TPT_PT_LANES == 1 || TPT_PT_LANES == 2 || TPT_PT_LANES == 4 || TPT_PT_LANES == 8 || TPT_PT_LANES == 16,
+              "Q must divide the wave");
+
 struct tpt_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -549,7 +479,7 @@ struct tpt_ctx {
     unsigned long long* counters = nullptr;
     unsigned* queue = nullptr;  // persistent gen: 8 shard counters, 64 B apart
     int num_cu = 0;
-    int pt_lanes = 8;  // Q: lanes per pixel of the PT kernel (1, 2, 4, 8, 16)
+    int pt_lanes = TPT_PT_LANES;  // Q: lanes per pixel of the PT kernel
     // wavefront BDPT state (sized for wf_cap pixels)
     void* wf_mem = nullptr;
     int64_t wf_cap = 0;
@@ -558,8 +488,6 @@ struct tpt_ctx {
     hipEvent_t ev_gen[2]{}, ev_fold[2]{};
     void* scan_tmp = nullptr;
     size_t scan_bytes = 0;
-    bool bdpt_mono = false;  // TPT_BDPT_KERNEL=mono: one lane per pixel stream (A/B only)
-    bool bdpt_serial = false;  // TPT_BDPT_SERIAL=1: connect/fold on the gen stream (per-kernel timing only)
 };
 
 namespace {
@@ -659,7 +587,7 @@ int launch(tpt_ctx* c, int mode, int spp, int64_t begin, int64_t stride, int64_t
     HIP_TRY(c, hipMemsetAsync(c->counters, 0, sizeof(unsigned long long) * 32, c->stream));
     HIP_TRY(c, hipEventRecord(c->ev0, c->stream));
     const bool lds = c->ds.lds_bytes > 0;
-    const size_t shmem = (size_t)c->ds.max_stack * kBlock * sizeof(int) + (size_t)c->ds.lds_bytes;
+    const size_t shmem = (size_t)c->ds.lds_bytes;
     if (mode == TPT_MODE_PT) {
         const int Q = c->pt_lanes;
         const int64_t qblocks = (count * Q + kBlock - 1) / kBlock;
@@ -677,7 +605,7 @@ int launch(tpt_ctx* c, int mode, int spp, int64_t begin, int64_t stride, int64_t
         else
             hipLaunchKernelGGL(tpt_pti_kernel<false>, dim3((unsigned)blocks), dim3(kBlock), shmem, c->stream, c->ds,
                                spp, begin, stride, count, dlist, drows, c->counters);
-    } else if (!c->bdpt_mono) {
+    } else {
         int rc = ensure_wf(c, count);
         if (rc) return rc;
         // Two streams: gen/scan/scatter of iteration it on c->stream, connect/fold on
@@ -685,7 +613,7 @@ int launch(tpt_ctx* c, int mode, int spp, int64_t begin, int64_t stride, int64_t
         // beside connect(it) and fills the tail of each.  Ordering per pixel is kept:
         // gen is sequential on one stream (RNG state), fold is sequential on the other
         // (acc, splat), and buffer b is rewritten by gen(it+2) only after fold(it).
-        hipStream_t s2 = c->bdpt_serial ? c->stream : c->stream2;
+        hipStream_t s2 = TPT_BDPT_SERIAL ? c->stream : c->stream2;
         HIP_TRY(c, hipEventRecord(c->ev_fold[0], c->stream));
         HIP_TRY(c, hipStreamWaitEvent(s2, c->ev_fold[0], 0));  // stream2 starts after ev0
         const unsigned pblocks = (unsigned)((count + kBlock - 1) / kBlock);
@@ -699,10 +627,6 @@ int launch(tpt_ctx* c, int mode, int spp, int64_t begin, int64_t stride, int64_t
         int64_t gb = (int64_t)std::max(per_cu, 1) * std::max(c->num_cu, 1);
         gb = std::min<int64_t>(gb, ((int64_t)pblocks + 7) / 8 * 8);
         const unsigned gblocks = (unsigned)std::max<int64_t>(8, gb / 8 * 8);
-        // connect walks the 4-wide shadow tree with a per-lane stack (shadow_q)
-        DScene dsc = c->ds;
-        dsc.max_stack = std::max(dsc.max_stack, dsc.q_stack);
-        const size_t cshmem = (size_t)dsc.max_stack * kBlock * sizeof(int) + (size_t)dsc.lds_bytes;
         const float inv = 1.0f / spp;
         for (int it = 0; it < spp; ++it) {
             const int b = it & 1;
@@ -731,10 +655,10 @@ int launch(tpt_ctx* c, int mode, int spp, int64_t begin, int64_t stride, int64_t
             HIP_TRY(c, hipEventRecord(c->ev_gen[b], c->stream));
             HIP_TRY(c, hipStreamWaitEvent(s2, c->ev_gen[b], 0));
             if (lds)
-                hipLaunchKernelGGL(tpt_bdpt_conn_kernel<true>, dim3(cblocks), dim3(kBlock), cshmem, s2, dsc, w,
+                hipLaunchKernelGGL(tpt_bdpt_conn_kernel<true>, dim3(cblocks), dim3(kBlock), shmem, s2, c->ds, w,
                                    dsplat);
             else
-                hipLaunchKernelGGL(tpt_bdpt_conn_kernel<false>, dim3(cblocks), dim3(kBlock), cshmem, s2, dsc,
+                hipLaunchKernelGGL(tpt_bdpt_conn_kernel<false>, dim3(cblocks), dim3(kBlock), shmem, s2, c->ds,
                                    w, dsplat);
             hipLaunchKernelGGL(tpt_bdpt_fold_kernel, dim3(pblocks), dim3(kBlock), 0, s2, w, inv);
             HIP_TRY(c, hipEventRecord(c->ev_fold[b], s2));
@@ -746,16 +670,6 @@ int launch(tpt_ctx* c, int mode, int spp, int64_t begin, int64_t stride, int64_t
         w.stride = stride;
         w.n = count;
         hipLaunchKernelGGL(tpt_bdpt_out_kernel, dim3(pblocks), dim3(kBlock), 0, c->stream, w, drows, dlist ? 1 : 0);
-    } else {
-        DScene dsc = c->ds;  // per-lane shadow_q needs the 4-wide tree's stack depth
-        dsc.max_stack = std::max(dsc.max_stack, dsc.q_stack);
-        const size_t cshmem = (size_t)dsc.max_stack * kBlock * sizeof(int) + (size_t)dsc.lds_bytes;
-        if (lds)
-            hipLaunchKernelGGL(tpt_bdpt_kernel<true>, dim3((unsigned)blocks), dim3(kBlock), cshmem, c->stream, dsc,
-                               spp, begin, stride, count, dlist, drows, dsplat, c->counters);
-        else
-            hipLaunchKernelGGL(tpt_bdpt_kernel<false>, dim3((unsigned)blocks), dim3(kBlock), cshmem, c->stream, dsc,
-                               spp, begin, stride, count, dlist, drows, dsplat, c->counters);
     }
     HIP_TRY(c, hipGetLastError());
     HIP_TRY(c, hipEventRecord(c->ev1, c->stream));
@@ -775,64 +689,6 @@ int launch(tpt_ctx* c, int mode, int spp, int64_t begin, int64_t stride, int64_t
         unsigned long long nb = 0;
         HIP_TRY(c, hipMemcpy(&nb, c->counters, sizeof(nb), hipMemcpyDeviceToHost));
         st->bounces = (int64_t)nb;
-    }
-    if (c->ds.dbg & 8) {  // BDPT phase stamps (TPT_DEBUG_FLAGS & 8)
-        unsigned long long d[8];
-        HIP_TRY(c, hipMemcpy(d, c->counters + 8, sizeof(d), hipMemcpyDeviceToHost));
-        double tot = (double)(d[1] + d[2] + d[3] + d[4]);
-        std::fprintf(stderr, "[tpt dbg] bdpt waves %llu cycles/wave %.4g: camera %.1f%% light %.1f%% rev %.1f%% connect %.1f%%\n",
-                     d[0], tot / d[0], 100.0 * d[1] / tot, 100.0 * d[2] / tot, 100.0 * d[3] / tot, 100.0 * d[4] / tot);
-    }
-    if (c->ds.dbg & 64) {
-        unsigned long long d[8];
-        HIP_TRY(c, hipMemcpy(d, c->counters + 8, sizeof(d), hipMemcpyDeviceToHost));
-        std::fprintf(stderr, "[tpt dbg] strategies %llu: s=0 %.1f%%, zero result %.1f%% (connecting and zero %.1f%%); "
-                     "shadow tests %.1f%% of strategies, %.1f%% of them shadowed\n",
-                     d[0], 100.0 * d[1] / d[0], 100.0 * d[2] / d[0], 100.0 * d[3] / d[0], 100.0 * d[4] / d[0],
-                     100.0 * d[5] / d[4]);
-    }
-    if (c->ds.dbg & 16) {
-        unsigned long long d[8];
-        HIP_TRY(c, hipMemcpy(d, c->counters + 8, sizeof(d), hipMemcpyDeviceToHost));
-        std::fprintf(stderr, "[tpt dbg] bdpt strategies per lane-sample: mean %.2f, wave-max %.2f\n",
-                     (double)d[5] / d[7], (double)d[6] / d[7]);
-    }
-#ifdef TPT_STAMPS
-    if (mode == TPT_MODE_BDPT) {
-        unsigned long long d[12];
-        HIP_TRY(c, hipMemcpy(d, c->counters + 16, sizeof(d), hipMemcpyDeviceToHost));
-        static const char* nm[8] = {"loop/decode", "loads", "shadow", "eval x2", "loop A", "loop B", "tail", "store/splat"};
-        double tot = 0;
-        for (int x = 0; x < 8; ++x) tot += (double)d[x];
-        for (int x = 0; x < 8; ++x) std::fprintf(stderr, "[tpt stamps] conn %-12s %5.1f%%\n", nm[x], 100.0 * d[x] / tot);
-    }
-    if (mode == TPT_MODE_PT) {
-        unsigned long long d[12];
-        HIP_TRY(c, hipMemcpy(d, c->counters + 16, sizeof(d), hipMemcpyDeviceToHost));
-        static const char* nm[12] = {"loop/fold", "mat_sample", "light sample", "bsdf light-hit", "bsdf geom",
-                                     "bsdf shadow", "bsdf eval", "mat_pdf", "light light-hit", "light shadow",
-                                     "light eval", "skip+tail"};
-        double tot = 0;
-        for (int x = 0; x < 12; ++x) tot += (double)d[x];
-        for (int x = 0; x < 12; ++x) std::fprintf(stderr, "[tpt stamps] %-16s %5.1f%%\n", nm[x], 100.0 * d[x] / tot);
-    }
-#endif
-    if (c->ds.dbg & 512) {
-        unsigned long long d = 0;
-        HIP_TRY(c, hipMemcpy(&d, c->counters + 8 + 6, sizeof(d), hipMemcpyDeviceToHost));
-        std::fprintf(stderr, "[tpt dbg] splat atomics %llu (%.2f per sample)\n", d, (double)d / (double)(count * spp));
-    }
-    if (c->ds.dbg & 128) {  // per-lane shadow walk census (TPT_DEBUG_FLAGS & 128)
-        unsigned long long d[4];
-        HIP_TRY(c, hipMemcpy(d, c->counters + 8, sizeof(d), hipMemcpyDeviceToHost));
-        std::fprintf(stderr, "[tpt dbg] shadow walks: wave calls %llu, lanes/call %.1f, steps/lane %.2f, wave steps/call %.2f\n",
-                     d[0], (double)d[1] / d[0], (double)d[2] / d[1], (double)d[3] / d[0]);
-    }
-    if (c->ds.dbg & 2) {  // profiling counters (TPT_DEBUG_FLAGS & 2)
-        unsigned long long d[8];
-        HIP_TRY(c, hipMemcpy(d, c->counters + 8, sizeof(d), hipMemcpyDeviceToHost));
-        std::fprintf(stderr, "[tpt dbg] shadow wave-calls %llu iters/call %.2f leaf-iters/call %.2f lanes/call %.1f\n",
-                     d[0], (double)d[1] / d[0], (double)d[3] / d[0], (double)d[5] / d[0]);
     }
     return TPT_OK;
 }
@@ -916,28 +772,22 @@ int tpt_upload_scene(tpt_ctx* c, const tpt_scene_desc* d) {
     HostScene hs;
     int rc = build_host_scene(d, hs, c->err);
     if (rc != TPT_OK) return rc;
-    if (hs.max_stack > kStackCap || hs.q_stack > kStackCap)
-        return fail(c, TPT_E_UNSUPPORTED, "BVH deeper than the LDS traversal stack (" + std::to_string(hs.max_stack) +
-                                              ", " + std::to_string(hs.q_stack) + ")");
     if (hs.nodes.size() > (size_t)0x7fffffff) return fail(c, TPT_E_UNSUPPORTED, "too many BVH nodes");
     // LDS staging (stage_scene): every array the traversals read when it all fits in
-    // 64 KB (the Cornell presets, ~8 KB: lds_full), else only the flat-query arrays --
+    // 64 KB (the Cornell presets, ~6 KB: lds_full), else only the flat-query arrays --
     // materials, leaves, groups and the flat leaves' triangles (the bunny scene,
     // ~2 KB) -- with the trees read through L2.  leaves[j].b indexes the triangle
     // array flat queries read: tris itself (full) or ftris (flat-only).
-    const char* no = std::getenv("TPT_NO_LDS");
-    const bool no_lds = no && no[0] == '1';
     const size_t mats16 = (hs.mats.size() * sizeof(DMat) + 15) & ~(size_t)15;
     const size_t lg = (hs.leaves.size() + hs.groups.size()) * sizeof(DNode);
-    const size_t full_b = hs.nodes.size() * sizeof(DNode) + hs.tris.size() * sizeof(DTri) + mats16 +
-                          hs.qnodes.size() * sizeof(DQNode) + lg;
+    const size_t full_b = hs.nodes.size() * sizeof(DNode) + hs.tris.size() * sizeof(DTri) + mats16 + lg;
     const size_t flat_b = mats16 + lg + hs.leaves.size() * sizeof(DTri);
     int lds_full = 0;
     size_t lds_b = 0;
-    if (!no_lds && full_b <= 64 * 1024) {
+    if (full_b <= 64 * 1024) {
         lds_full = 1;
         lds_b = full_b;
-    } else if (!no_lds && hs.leaves.size() <= (size_t)kFlatMaxLeaves && flat_b <= 64 * 1024) {
+    } else if (hs.leaves.size() <= (size_t)kFlatMaxLeaves && flat_b <= 64 * 1024) {
         lds_b = flat_b;
     }
     hs.ftris.clear();
@@ -958,7 +808,7 @@ int tpt_upload_scene(tpt_ctx* c, const tpt_scene_desc* d) {
     size_t o_nodes = push_array(blob, hs.nodes), o_area = push_array(blob, hs.node_area),
            o_tris = push_array(blob, hs.tris), o_trix = push_array(blob, hs.trix), o_sph = push_array(blob, hs.sph),
            o_mats = push_array(blob, hs.mats), o_objs = push_array(blob, hs.objs),
-           o_em = push_array(blob, hs.emitters), o_q = push_array(blob, hs.qnodes), o_t = push_array(blob, hs.tnodes),
+           o_em = push_array(blob, hs.emitters), o_t = push_array(blob, hs.tnodes),
            o_lf = push_array(blob, hs.leaves), o_gr = push_array(blob, hs.groups), o_ft = push_array(blob, hs.ftris);
     if (c->blob) { (void)hipFree(c->blob); c->blob = nullptr; }
     HIP_TRY(c, hipMalloc(&c->blob, blob.size()));
@@ -974,7 +824,6 @@ int tpt_upload_scene(tpt_ctx* c, const tpt_scene_desc* d) {
     ds.mats = (const DMat*)(b + o_mats);
     ds.objs = (const DObj*)(b + o_objs);
     ds.emitters = (const int32_t*)(b + o_em);
-    ds.qnodes = (const DQNode*)(b + o_q);
     ds.tnodes = (const DNode*)(b + o_t);
     ds.leaves = (const DNode*)(b + o_lf);
     ds.nleaf = (int)hs.leaves.size();
@@ -982,7 +831,6 @@ int tpt_upload_scene(tpt_ctx* c, const tpt_scene_desc* d) {
     ds.ngroup = (int)hs.groups.size();
     ds.ftris = lds_full ? ds.tris : (const DTri*)(b + o_ft);
     ds.lds_full = lds_full;
-    ds.nqnodes = (int)hs.qnodes.size();
     ds.nmats = (int)hs.mats.size();
     ds.n_emitters = (int)hs.emitters.size();
     // BVHAccel::Sample (1 draw) + Triangle::Sample (2) per mesh emitter, Sphere::Sample (2)
@@ -996,27 +844,12 @@ int tpt_upload_scene(tpt_ctx* c, const tpt_scene_desc* d) {
     ds.height = hs.height;
     ds.scale = camera_scale(hs.fov);
     for (int k = 0; k < 3; ++k) { ds.eye[k] = hs.eye[k]; ds.bg[k] = hs.bg[k]; }
-    // Per-lane walks are stackless (threaded tree); only the per-lane 4-wide shadow
-    // walk (TPT_LANE_SHADOW == 1, A/B builds) keeps an LDS stack.
-    ds.max_stack = TPT_LANE_SHADOW == 1 ? hs.max_stack : 0;
-    ds.q_stack = TPT_LANE_SHADOW == 1 ? hs.q_stack : 0;
-    {
-        ds.lds_bytes = (int)lds_b;
-        const char* dbg = std::getenv("TPT_DEBUG_FLAGS");
-        ds.dbg = dbg ? std::atoi(dbg) : 0;
-        ds.dbgc = c->counters + 8;
-        const char* bk = std::getenv("TPT_BDPT_KERNEL");
-        c->bdpt_mono = bk && bk[0] == 'm';
-        const char* ser = std::getenv("TPT_BDPT_SERIAL");
-        c->bdpt_serial = ser && ser[0] == '1';
-        // flat (all-leaves) queries for small scenes; TPT_FLAT overrides the bits (A/B)
-        const char* fl = std::getenv("TPT_FLAT");
-        ds.flat = fl ? std::atoi(fl) : TPT_FLAT_DEFAULT;
-        if (ds.nleaf > kFlatMaxLeaves || ds.lds_bytes == 0) ds.flat = 0;
-        const char* q = std::getenv("TPT_PT_LANES");
-        c->pt_lanes = q ? std::atoi(q) : 8;  // Q = 8 measured best on one MI355X (Standard, 1024 spp)
-        if (c->pt_lanes != 1 && c->pt_lanes != 2 && c->pt_lanes != 4 && c->pt_lanes != 8 && c->pt_lanes != 16) c->pt_lanes = 1;
-    }
+    ds.lds_bytes = (int)lds_b;
+    // flat (all-leaves) queries for small scenes; TPT_FLAT overrides the bits: 0 walks
+    // the threaded tree everywhere (the cross-check tests/test_gpu_parity.py runs)
+    const char* fl = std::getenv("TPT_FLAT");
+    ds.flat = fl ? std::atoi(fl) : TPT_FLAT_DEFAULT;
+    if (ds.nleaf > kFlatMaxLeaves || ds.lds_bytes == 0) ds.flat = 0;
     c->ds = ds;
     c->hs = std::move(hs);
     c->has_scene = true;
@@ -1098,8 +931,8 @@ int tpt_intersect(tpt_ctx* c, const float* rays, int64_t n, int32_t cull, float*
     int rc = TPT_OK;
     if (hipMemcpy(dr, rays, n * 6 * sizeof(float), hipMemcpyHostToDevice) != hipSuccess) rc = TPT_E_DEVICE;
     if (!rc) {
-        hipLaunchKernelGGL(tpt_intersect_kernel, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock),
-                           (size_t)c->ds.max_stack * kBlock * sizeof(int), c->stream, c->ds, dr, n, cull, dout);
+        hipLaunchKernelGGL(tpt_intersect_kernel, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                           c->stream, c->ds, dr, n, cull, dout);
         if (hipGetLastError() != hipSuccess || hipStreamSynchronize(c->stream) != hipSuccess ||
             hipMemcpy(out, dout, n * 8 * sizeof(float), hipMemcpyDeviceToHost) != hipSuccess)
             rc = TPT_E_DEVICE;

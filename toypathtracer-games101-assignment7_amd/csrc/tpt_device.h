@@ -4,10 +4,9 @@
 // follows the numerics contract of tpt_devmath.h (kernels are built with
 // -ffp-contract=off).
 //
-// Memory model: the scene (tpt_scene.h) is read through the L1/L2 (it is a few KB
-// for the Cornell presets, <1 MB with the bunny); the per-lane BVH stack lives in
-// LDS in a [depth][lane] layout so that ds_read/ds_write_b32 from a wave never
-// bank-conflict (bank = lane mod 32 whatever the per-lane depth).
+// Memory model: the scene (tpt_scene.h) is staged in LDS when it fits (the Cornell
+// presets, a few KB) and read through L1/L2 otherwise (the bunny mesh, <1 MB); ray
+// queries are stackless (flat all-leaves loops or threaded-tree walks).
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -21,16 +20,6 @@ namespace tpt {
 #define TPT_D __device__ __forceinline__
 
 constexpr int kBlock = 256;     // threads per workgroup (4 waves)
-// Segment culling for shadow walks (skip nodes whose box misses the padded AABB of
-// the shadow segment) is OFF: it assumes a computed hit point stays within the pad
-// of its triangle's box, but Moller-Trumbore's f32 cross products can move t by
-// ~2^-23 |tvec||e1||e2| / |det| on grazing rays, which no fixed pad bounds.  It
-// bought ~1.4 %.  Kept for A/B builds only (-DTPT_SEGMENT_CULL=1).
-#ifndef TPT_SEGMENT_CULL
-#define TPT_SEGMENT_CULL 0
-#endif
-constexpr int kStackCap = 64;   // max LDS stack entries per lane / per wave packet (upload rejects deeper trees)
-
 // ------------------------------------------------------------------ rays --
 struct Ray {
     V3 o, d, inv;
@@ -76,9 +65,6 @@ TPT_D bool slab_hit(float x0, float y0, float z0, float x1, float y1, float z1, 
 TPT_D bool box_hit(const DNode& n, const Ray& r) {
     return slab_hit(n.bmin[0], n.bmin[1], n.bmin[2], n.bmax[0], n.bmax[1], n.bmax[2], r);
 }
-TPT_D bool box_hit_q(const DQNode& q, int j, const Ray& r) {
-    return slab_hit(q.bmin[0][j], q.bmin[1][j], q.bmin[2][j], q.bmax[0][j], q.bmax[1][j], q.bmax[2][j], r);
-}
 // slab_hit for a ray with finite inv (ray_monotone): (b - o) * inv is then never
 // NaN, so std::max/std::min equal the hardware max/min and the swap is a min/max
 // pair (a +-0 difference cannot change `nmax > 0` or `nmin <= nmax`).  Same
@@ -91,9 +77,6 @@ TPT_D bool slab_hit_finite(float x0, float y0, float z0, float x1, float y1, flo
     const float nmax = fminf(fminf(3.40282347e+38f, fmaxf(ax, bx)), fminf(fmaxf(ay, by), fmaxf(az, bz)));
     return (nmax > 0.0f) & (nmin <= nmax);
 }
-TPT_D bool box_hit_q_finite(const DQNode& q, int j, const Ray& r) {
-    return slab_hit_finite(q.bmin[0][j], q.bmin[1][j], q.bmin[2][j], q.bmax[0][j], q.bmax[1][j], q.bmax[2][j], r);
-}
 // kFin: every ray of the (sub)wave has a finite inv (wave_finite), so the NaN-free
 // form gives the same decision.
 template <bool kFin>
@@ -102,10 +85,11 @@ TPT_D bool box_hit_t(const DNode& n, const Ray& r) {
                 : slab_hit(n.bmin[0], n.bmin[1], n.bmin[2], n.bmax[0], n.bmax[1], n.bmax[2], r);
 }
 
-// The slab test is monotone in the box bounds (tpt_scene_build.cpp: build_q) unless
-// a direction component is +-0 or tiny enough that 1/d overflows: with inv = -inf
-// a box flat at o.x passes while a box [o.x, o.x + w] does not.  Rays with an
-// infinite inv component are walked on the binary tree instead.
+// The slab test (Bounds3::IntersectP) is monotone in the box bounds -- fl(b - o) and
+// fl(x * inv) are monotone in b and std::max / std::min preserve order -- unless a
+// direction component is +-0 or tiny enough that 1/d overflows: with inv = -inf a
+// box flat at o.x passes while a box [o.x, o.x + w] does not.  Rays with an infinite
+// inv component are walked on the threaded tree instead.
 TPT_D bool ray_monotone(const Ray& r) {
     const float inf = 3.40282347e+38f;
     return fabs_(r.inv.x) <= inf && fabs_(r.inv.y) <= inf && fabs_(r.inv.z) <= inf;
@@ -176,7 +160,7 @@ TPT_D bool sphere_test(const DSphere& s, const Ray& r, int cull, double& dist) {
 // (tpt_scene.h).  Same pop order (right child first), strict `>` on the f64
 // distance, so ties resolve exactly as in the reference.
 template <bool kFin>
-TPT_D Hit traverse_t(const DScene& s, int root, const Ray& r, int cull, int* /*stk*/) {
+TPT_D Hit traverse_t(const DScene& s, int root, const Ray& r, int cull) {
     // stackless walk of the threaded tree (tpt_scene.h): one node fetch per step
     Hit best;
     best.prim = -1;
@@ -210,8 +194,8 @@ TPT_D Hit traverse_t(const DScene& s, int root, const Ray& r, int cull, int* /*s
     return best;
 }
 // ---- flat queries: every primitive leaf box, no interior nodes ----------------
-// For a ray with finite inv the slab test is monotone in the box bounds (build_q in
-// tpt_scene_build.cpp) and every interior box is the union of its children's
+// For a ray with finite inv the slab test is monotone in the box bounds (see
+// ray_monotone) and every interior box is the union of its children's
 // (BVH.cpp:58-98), so a leaf's box passing implies every ancestor's box passes: the
 // primitives the reference tests are exactly those whose own leaf box passes.
 // Testing all leaf boxes in the reference's DFS leaf order (HostScene::leaves)
@@ -221,7 +205,7 @@ TPT_D Hit traverse_t(const DScene& s, int root, const Ray& r, int cull, int* /*s
 // when some lane's box passed.  For scenes with few leaves (the Cornell presets: 32
 // triangles) this beats a per-lane walk; rays with an infinite inv component keep
 // the walk.
-enum { kFlatShadow = 1, kFlatHit = 2, kFlatPkShadow = 4 };
+enum { kFlatShadow = 1, kFlatHit = 2 };  // DScene::flat bits
 // A walk group (groups[g].b < 0) is a mesh too large for the flat list (the bunny):
 // a lane whose ray passed the group box -- the mesh root's box, tpt_scene.h -- walks
 // the mesh's threaded subtree from the root's right child (a) until kMeshExit, i.e.
@@ -329,10 +313,10 @@ TPT_D bool shadow_flat(const DScene& s, const Ray& r, V3 lc, double thr, int cul
     return sh;
 }
 
-TPT_D Hit traverse(const DScene& s, int root, const Ray& r, int cull, int* stk) {
+TPT_D Hit traverse(const DScene& s, int root, const Ray& r, int cull) {
     const bool fin = wave_finite(r);
     if (fin && root == 0 && (s.flat & kFlatHit)) return traverse_flat(s, r, cull);
-    return fin ? traverse_t<true>(s, root, r, cull, stk) : traverse_t<false>(s, root, r, cull, stk);
+    return fin ? traverse_t<true>(s, root, r, cull) : traverse_t<false>(s, root, r, cull);
 }
 
 // Intersection fields of a hit (Triangle.cpp:109-114, Sphere.cpp:30-36)
@@ -366,8 +350,8 @@ TPT_D PTV ptv_bg() {
     return v;
 }
 // Scene::Intersect (Scene.cpp:21-35)
-TPT_D PTV scene_intersect(const DScene& s, const Ray& r, int cull, int* stk) {
-    Hit h = traverse(s, 0, r, cull, stk);
+TPT_D PTV scene_intersect(const DScene& s, const Ray& r, int cull) {
+    Hit h = traverse(s, 0, r, cull);
     PTV v = ptv_bg();
     if (h.prim >= 0) {
         hit_geometry(s, r, h, v.x, v.N);
@@ -376,46 +360,22 @@ TPT_D PTV scene_intersect(const DScene& s, const Ray& r, int cull, int* stk) {
     }
     return v;
 }
+TPT_D int lane_id() { return __lane_id(); }
+
 // Scene::ShadowCheck(Vector3f, Vector3f, FaceCulling) (Scene.cpp:37-48):
 // shadowed iff the CLOSEST hit of the ray lc -> x has |hit - lc|^2 < |x - lc|^2 - 1.
 // The hit point is lc + float(t)*d rounded per component and its squared distance
 // is summed in double: every step is monotone, so d2(t) is non-decreasing in t and
 // "closest hit's d2 < thr"  <=>  "some reachable hit's d2 < thr".  Hence an any-hit
 // traversal with early exit is exact.  Box tests are the reference's, so the set
-// of reachable primitives is unchanged (segment culling: see TPT_SEGMENT_CULL).
-// Culling box of a shadow segment (TPT_SEGMENT_CULL, A/B only): everything when off.
-TPT_D void segment_box(const Ray& r, double thr, V3& lo, V3& hi) {
-#if TPT_SEGMENT_CULL
-    const float T = sqrt_f((float)(thr > 0.0 ? thr : 0.0)) * 1.0002f + 0.02f;
-    const V3 e = v3(r.o.x + T * r.d.x, r.o.y + T * r.d.y, r.o.z + T * r.d.z);
-    const float pad = 0.01f + 1e-4f * T;
-    lo = v3(fminf(r.o.x, e.x) - pad, fminf(r.o.y, e.y) - pad, fminf(r.o.z, e.z) - pad);
-    hi = v3(fmaxf(r.o.x, e.x) + pad, fmaxf(r.o.y, e.y) + pad, fmaxf(r.o.z, e.z) + pad);
-#else
-    (void)r;
-    (void)thr;
-    lo = v3s(-3.40282347e+38f);
-    hi = v3s(3.40282347e+38f);
-#endif
-}
-TPT_D bool box_overlap(const DNode& n, V3 lo, V3 hi) {
-    return !((n.bmin[0] > hi.x) | (n.bmax[0] < lo.x) | (n.bmin[1] > hi.y) | (n.bmax[1] < lo.y) | (n.bmin[2] > hi.z) |
-             (n.bmax[2] < lo.z));
-}
-// Branch-free (bitwise) so the six compares never become a chain of branches.
-TPT_D bool box_overlap_q(const DQNode& q, int j, V3 lo, V3 hi) {
-    return !((q.bmin[0][j] > hi.x) | (q.bmax[0][j] < lo.x) | (q.bmin[1][j] > hi.y) | (q.bmax[1][j] < lo.y) |
-             (q.bmin[2][j] > hi.z) | (q.bmax[2][j] < lo.z));
-}
+// of reachable primitives is unchanged.
 template <bool kFin>
-TPT_D bool shadow_pts_walk(const DScene& s, const Ray& r, V3 lc, double thr, V3 lo, V3 hi, int cull, int* /*stk*/,
-                           int& steps) {
+TPT_D bool shadow_walk(const DScene& s, const Ray& r, V3 lc, double thr, int cull) {
     int cur = 0, cont = kWalkEnd;
     while (cur >= 0) {
-        ++steps;
         const DNode n = s.tnodes[cur];
         int nxt = n.b;
-        if (box_overlap(n, lo, hi) & box_hit_t<kFin>(n, r)) {
+        if (box_hit_t<kFin>(n, r)) {
             if (n.a >= 0) {
                 if (n.a & kSpliceBit) {
                     cont = n.b;
@@ -439,336 +399,16 @@ TPT_D bool shadow_pts_walk(const DScene& s, const Ray& r, V3 lc, double thr, V3 
     }
     return false;
 }
-TPT_D bool shadow_pts(const DScene& s, V3 lc, V3 x, int cull, int* stk) {
-    if (s.dbg & 1) return false;  // profiling ablation only
+// The shadow query of Scene::ShadowCheck from lc toward x: flat all-leaves query
+// when every ray of the wave has a finite inv, else a per-lane threaded walk.
+TPT_D bool shadow_ray(const DScene& s, V3 lc, V3 x, int cull) {
     const double ld2 = dot3(lc - x, lc - x);
     const double thr = ld2 - 1.0f;
-    if (!(thr > 0.0)) return false;  // d2 >= 0 can never be < thr
+    if (!(thr > 0.0)) return false;  // d2 >= 0 can never be < thr (the lane leaves the wave's query)
     const Ray r = make_ray(lc, normalized(x - lc));
-    V3 lo, hi;
-    segment_box(r, thr, lo, hi);
-    int steps = 0;
     const bool fin = wave_finite(r);
     if (fin && (s.flat & kFlatShadow)) return shadow_flat(s, r, lc, thr, cull);
-    const bool sh = fin ? shadow_pts_walk<true>(s, r, lc, thr, lo, hi, cull, stk, steps)
-                        : shadow_pts_walk<false>(s, r, lc, thr, lo, hi, cull, stk, steps);
-    if (s.dbg & 128) {  // walk census: wave calls, active lanes, lane steps, wave steps (max over lanes)
-        int mx = steps;
-        for (int o = 32; o >= 1; o >>= 1) mx = max(mx, __shfl_xor(mx, o));
-        const unsigned long long act = __ballot(1);
-        atomicAdd(s.dbgc + 2, (unsigned long long)steps);
-        if ((int)__lane_id() == __builtin_ctzll(act)) {
-            atomicAdd(s.dbgc + 0, 1ull);
-            atomicAdd(s.dbgc + 1, (unsigned long long)__popcll(act));
-            atomicAdd(s.dbgc + 3, (unsigned long long)mx);
-        }
-    }
-    return sh;
-}
-
-// shadow_pts on the 4-wide tree (same answer, see build_q): one node fetch and four
-// box tests per step instead of one fetch per box.
-TPT_D bool shadow_q(const DScene& s, V3 lc, V3 x, int cull, int* stk) {
-    if (s.dbg & 1) return false;  // profiling ablation only
-    const double ld2 = dot3(lc - x, lc - x);
-    const double thr = ld2 - 1.0f;
-    if (!(thr > 0.0)) return false;  // d2 >= 0 can never be < thr
-    const Ray r = make_ray(lc, normalized(x - lc));
-    if (!ray_monotone(r)) return shadow_pts(s, lc, x, cull, stk);
-    V3 lo, hi;
-    segment_box(r, thr, lo, hi);
-    int sp = 1;
-    stk[0] = 0;
-    while (sp > 0) {
-        --sp;
-        const DQNode q = s.qnodes[stk[sp * kBlock]];
-        bool hit[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-            hit[j] = (q.child[j] != kEmptyLeaf) & box_overlap_q(q, j, lo, hi) & box_hit_q_finite(q, j, r);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int c = q.child[j];
-            if (!hit[j]) continue;
-            if (c >= 0) {
-                stk[sp * kBlock] = c;
-                ++sp;
-                continue;
-            }
-            const int prim = -1 - c;
-            double dist;
-            bool h;
-            if (prim < s.ntri) h = tri_test(s.tris[prim], r, cull, dist);
-            else h = sphere_test(s.sph[prim - s.ntri], r, cull, dist);
-            if (h) {
-                const V3 hx = r.o + mul(r.d, (float)dist);
-                if (dot3(hx - lc, hx - lc) < thr) return true;
-            }
-        }
-    }
-    return false;
-}
-
-// ------------------------------------------------------- wave packets --
-// Wave-packet traversal: the 64 lanes of a wave walk ONE depth-first node sequence
-// (reference order: right child popped first) held in a wave-uniform LDS stack of
-// {node, lane mask}.  A lane's mask bit is set on a node iff every ancestor box
-// passed that lane's ray test (BVH.cpp:121-137 pushes children of a node whose
-// box passed), so each lane evaluates exactly the boxes and primitives the
-// reference evaluates for its ray, in the same relative order.  Node fetches are
-// wave-uniform (LDS broadcast / scalar loads), the per-iteration cost is one box
-// test, and a primitive test runs only on iterations that are leaves, with the
-// lanes that reached that leaf -- instead of every lane paying for the leaf test of
-// whichever lane happens to be at a leaf.
-struct Packet {
-    int* node;                  // [kStackCap] wave-uniform stack, LDS
-    unsigned long long* mask;   // [kStackCap]
-};
-TPT_D int lane_id() { return __lane_id(); }
-TPT_D int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
-TPT_D unsigned long long uni64(unsigned long long v) {
-    const unsigned lo = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)v);
-    const unsigned hi = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(v >> 32));
-    return ((unsigned long long)hi << 32) | lo;
-}
-
-// Packet form of shadow_pts (same decision per lane, see the exactness note there).
-// Children are box-tested together at their parent (both tests are independent,
-// so they overlap in the pipeline) and the walk descends without a stack round
-// trip; a node's mask holds the lanes whose ray passed that node's own box.
-TPT_D bool shadow_pts_packet(const DScene& s, V3 lc, V3 x, int cull, Packet pk, bool active = true) {
-    const double ld2 = dot3(lc - x, lc - x);
-    const double thr = ld2 - 1.0f;
-    bool done = !active || !(thr > 0.0);  // done lanes have their answer in `shadowed`
-    bool shadowed = false;
-    if (s.dbg & 1) done = true;  // profiling ablation only
-    const Ray r = make_ray(lc, normalized(x - lc));
-    V3 lo, hi;
-    segment_box(r, thr, lo, hi);
-    unsigned long long live = uni64(__ballot(!done));
-    if (live == 0) return shadowed;
-    unsigned long long it_all = 0, it_leaf = 0;
-    int sp = 0;
-    int cur = 0;
-    unsigned long long m;
-    {
-        const DNode n = s.nodes[0];
-        m = uni64(__ballot(!done & box_overlap(n, lo, hi) & box_hit(n, r)));
-    }
-    for (;;) {
-        ++it_all;
-        if (m != 0) {
-            const DNode n = s.nodes[cur];
-            if (n.a >= 0) {
-                const DNode L = s.nodes[n.a];
-                const DNode R = s.nodes[n.b];
-                const bool mine = (m >> lane_id()) & 1ull;
-                const bool hl = mine & box_overlap(L, lo, hi) & box_hit(L, r);
-                const bool hr = mine & box_overlap(R, lo, hi) & box_hit(R, r);
-                const unsigned long long ml = uni64(__ballot(hl)), mr = uni64(__ballot(hr));
-                if (mr != 0) {  // right subtree first (BVH.cpp:129-132), left deferred
-                    if (ml != 0) {
-                        if (lane_id() == __builtin_ctzll(ml)) { pk.node[sp] = n.a; pk.mask[sp] = ml; }
-                        ++sp;
-                    }
-                    cur = n.b;
-                    m = mr;
-                    continue;
-                }
-                if (ml != 0) { cur = n.a; m = ml; continue; }
-            } else if (n.a != kEmptyLeaf) {
-                ++it_leaf;
-                if ((m >> lane_id()) & 1ull) {
-                    const int prim = -1 - n.a;
-                    double dist;
-                    bool h;
-                    if (prim < s.ntri) h = tri_test(s.tris[prim], r, cull, dist);
-                    else h = sphere_test(s.sph[prim - s.ntri], r, cull, dist);
-                    if (h) {
-                        const V3 hx = r.o + mul(r.d, (float)dist);
-                        if (dot3(hx - lc, hx - lc) < thr) { shadowed = true; done = true; }
-                    }
-                }
-                live = uni64(__ballot(!done)) & live;
-                if (live == 0) break;
-            }
-        }
-        if (sp == 0) break;
-        --sp;
-        cur = uni(pk.node[sp]);
-        m = uni64(pk.mask[sp]) & live;
-    }
-    if (s.dbg & 2) {
-        const unsigned long long act = __ballot(1);
-        if (lane_id() == __builtin_ctzll(act)) {
-            atomicAdd(s.dbgc + 0, 1ull);
-            atomicAdd(s.dbgc + 1, it_all);
-            atomicAdd(s.dbgc + 2, it_all);
-            atomicAdd(s.dbgc + 3, it_leaf);
-            atomicAdd(s.dbgc + 5, (unsigned long long)__popcll(act));
-        }
-    }
-    return shadowed;
-}
-
-// shadow_pts_packet on the 4-wide tree (same answer per lane, see build_q): per step
-// one wave-uniform node fetch, four box tests per lane, leaf children tested by the
-// lanes whose box passed, interior children pushed with their lane masks.  Lanes
-// whose ray is not monotone (ray_monotone) take the binary walk afterwards.
-TPT_D bool shadow_q_packet(const DScene& s, V3 lc, V3 x, int cull, Packet pk) {
-    const double ld2 = dot3(lc - x, lc - x);
-    const double thr = ld2 - 1.0f;
-    bool done = !(thr > 0.0);  // done lanes have their answer in `shadowed`
-    bool shadowed = false;
-    if (s.dbg & 1) done = true;  // profiling ablation only
-    const Ray r = make_ray(lc, normalized(x - lc));
-    if ((s.flat & kFlatPkShadow) && wave_finite(r)) {
-        if (!done) shadowed = shadow_flat(s, r, lc, thr, cull);
-        return shadowed;
-    }
-    const bool slow = !done && !ray_monotone(r);
-    if (slow) done = true;
-    V3 lo, hi;
-    segment_box(r, thr, lo, hi);
-    unsigned long long live = uni64(__ballot(!done));
-    unsigned long long it_all = 0, it_leaf = 0;
-    if (live != 0) {
-        int sp = 0;
-        int cur = 0;
-        unsigned long long m = live;
-        for (;;) {
-            if (m != 0) {
-                ++it_all;
-                const DQNode q = s.qnodes[cur];  // one 128-B fetch, all loads in flight together
-                const bool mine = (m >> lane_id()) & 1ull;
-                unsigned long long mk[4];
-                int ch[4];
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    ch[j] = uni(q.child[j]);
-                    const bool h = mine & (ch[j] != kEmptyLeaf) & box_overlap_q(q, j, lo, hi) & box_hit_q_finite(q, j, r);
-                    mk[j] = uni64(__ballot(h));
-                }
-                int next = 0;
-                unsigned long long nm = 0;
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    if (mk[j] == 0) continue;
-                    if (ch[j] < 0) {
-                        ++it_leaf;
-#ifdef TPT_ABL_NOLEAF
-                        if (false) {
-#else
-                        if (((mk[j] >> lane_id()) & 1ull) && !done) {
-#endif
-                            const int prim = -1 - ch[j];
-                            double dist;
-                            bool h;
-                            if (prim < s.ntri) h = tri_test(s.tris[prim], r, cull, dist);
-                            else h = sphere_test(s.sph[prim - s.ntri], r, cull, dist);
-                            if (h) {
-                                const V3 hx = r.o + mul(r.d, (float)dist);
-                                if (dot3(hx - lc, hx - lc) < thr) { shadowed = true; done = true; }
-                            }
-                        }
-                        live = uni64(__ballot(!done)) & live;
-                    } else if (nm == 0) {
-                        next = ch[j];
-                        nm = mk[j];
-                    } else {
-                        if (lane_id() == __builtin_ctzll(mk[j])) { pk.node[sp] = ch[j]; pk.mask[sp] = mk[j]; }
-                        ++sp;
-                    }
-                }
-                if (live == 0) break;
-                if (nm != 0) { cur = next; m = nm & live; continue; }
-            }
-            if (sp == 0) break;
-            --sp;
-            cur = uni(pk.node[sp]);
-            m = uni64(pk.mask[sp]) & live;
-        }
-    }
-    if (s.dbg & 2) {
-        const unsigned long long act = __ballot(1);
-        if (lane_id() == __builtin_ctzll(act)) {
-            atomicAdd(s.dbgc + 0, 1ull);
-            atomicAdd(s.dbgc + 1, it_all);
-            atomicAdd(s.dbgc + 3, it_leaf);
-            atomicAdd(s.dbgc + 5, (unsigned long long)__popcll(act));
-        }
-    }
-    if (uni64(__ballot(slow)) != 0) {
-        const bool sh = shadow_pts_packet(s, lc, x, cull, pk, slow);
-        if (slow) shadowed = sh;
-    }
-    return shadowed;
-}
-
-// Packet closest hit (BVHAccel::Intersect semantics per lane: same boxes, same
-// leaf order, strict `>` on the f64 distance).  `root` must be wave-uniform; `cull`
-// may differ per lane.  Inactive lanes (active == false) take no part.
-TPT_D Hit traverse_packet(const DScene& s, int root, const Ray& r, int cull, Packet pk, bool active) {
-    Hit best;
-    best.prim = -1;
-    best.dist = 0.0;
-    if (root < 0) return best;
-    int sp = 0;
-    int cur = root;
-    unsigned long long m;
-    {
-        const DNode n = s.nodes[root];
-        m = uni64(__ballot(active && box_hit(n, r)));
-    }
-    for (;;) {
-        if (m != 0) {
-            const DNode n = s.nodes[cur];
-            if (n.a >= 0) {
-                const DNode L = s.nodes[n.a];
-                const DNode R = s.nodes[n.b];
-                const bool mine = (m >> lane_id()) & 1ull;
-                const bool hl = mine & box_hit(L, r);
-                const bool hr = mine & box_hit(R, r);
-                const unsigned long long ml = uni64(__ballot(hl)), mr = uni64(__ballot(hr));
-                if (mr != 0) {
-                    if (ml != 0) {
-                        if (lane_id() == __builtin_ctzll(ml)) { pk.node[sp] = n.a; pk.mask[sp] = ml; }
-                        ++sp;
-                    }
-                    cur = n.b;
-                    m = mr;
-                    continue;
-                }
-                if (ml != 0) { cur = n.a; m = ml; continue; }
-            } else if (n.a != kEmptyLeaf) {
-                if ((m >> lane_id()) & 1ull) {
-                    const int prim = -1 - n.a;
-                    double dist;
-                    bool h;
-                    if (prim < s.ntri) h = tri_test(s.tris[prim], r, cull, dist);
-                    else h = sphere_test(s.sph[prim - s.ntri], r, cull, dist);
-                    if (h && (best.prim < 0 || best.dist > dist)) { best.dist = dist; best.prim = prim; }
-                }
-            }
-        }
-        if (sp == 0) break;
-        --sp;
-        cur = uni(pk.node[sp]);
-        m = uni64(pk.mask[sp]);
-    }
-    return best;
-}
-// Scene::Intersect (Scene.cpp:21-35), packet form.
-TPT_D Hit traverse(const DScene& s, int root, const Ray& r, int cull, int* stk);
-TPT_D PTV scene_intersect_packet(const DScene& s, const Ray& r, int cull, Packet pk, bool active = true) {
-    Hit h = traverse_packet(s, 0, r, cull, pk, active);
-    PTV v = ptv_bg();
-    if (h.prim >= 0) {
-        hit_geometry(s, r, h, v.x, v.N);
-        v.type = T_MID;
-        v.prim = h.prim;
-    }
-    return v;
+    return fin ? shadow_walk<true>(s, r, lc, thr, cull) : shadow_walk<false>(s, r, lc, thr, cull);
 }
 
 // ------------------------------------------------------------ materials --
@@ -1175,7 +815,7 @@ struct Hit2 {
 // NoCull and CullBack closest hits of one ray against one emitter object, one
 // traversal (same node order, same strict `>` tie rule for each result).
 template <bool kFin>
-TPT_D void mesh_hit_nocull_back(const DScene& s, int root, const Ray& r, Hit& hn, Hit& hb, int* /*stk*/) {
+TPT_D void mesh_hit_nocull_back(const DScene& s, int root, const Ray& r, Hit& hn, Hit& hb) {
     int cur = root;  // a mesh subtree ends in kMeshExit
     while (cur >= 0) {
         const DNode n = s.tnodes[cur];
@@ -1196,7 +836,7 @@ TPT_D void mesh_hit_nocull_back(const DScene& s, int root, const Ray& r, Hit& hn
         cur = nxt;
     }
 }
-TPT_D void object_hit_nocull_back(const DScene& s, const DObj& o, const Ray& r, Hit& hn, Hit& hb, int* stk) {
+TPT_D void object_hit_nocull_back(const DScene& s, const DObj& o, const Ray& r, Hit& hn, Hit& hb) {
     hn.prim = hb.prim = -1;
     hn.dist = hb.dist = 0.0;
     if (o.kind != TPT_OBJ_MESH) {
@@ -1207,12 +847,12 @@ TPT_D void object_hit_nocull_back(const DScene& s, const DObj& o, const Ray& r, 
         return;
     }
     if (o.root < 0) return;
-    if (wave_finite(r)) mesh_hit_nocull_back<true>(s, o.root, r, hn, hb, stk);
-    else mesh_hit_nocull_back<false>(s, o.root, r, hn, hb, stk);
+    if (wave_finite(r)) mesh_hit_nocull_back<true>(s, o.root, r, hn, hb);
+    else mesh_hit_nocull_back<false>(s, o.root, r, hn, hb);
 }
 
-TPT_D Hit object_hit(const DScene& s, const DObj& o, const Ray& r, int cull, int* stk) {
-    if (o.kind == TPT_OBJ_MESH) return traverse(s, o.root, r, cull, stk);
+TPT_D Hit object_hit(const DScene& s, const DObj& o, const Ray& r, int cull) {
+    if (o.kind == TPT_OBJ_MESH) return traverse(s, o.root, r, cull);
     Hit h;
     h.prim = -1;
     h.dist = 0.0;
@@ -1222,35 +862,6 @@ TPT_D Hit object_hit(const DScene& s, const DObj& o, const Ray& r, int cull, int
 }
 
 // ------------------------------------------------------------------- PT ---
-// Diagnostic build only (-DTPT_STAMPS): wave-level s_memtime stamps that add the
-// cycles of each section of a PT sample into scalar sums, stored once per wave
-// into DScene::dbgc[16..].  Production builds compile these to nothing.
-#ifdef TPT_STAMPS
-struct Stamps {
-    unsigned long long last, acc[12];
-};
-TPT_D unsigned long long stamp_now() {
-    unsigned long long t;
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-    __builtin_amdgcn_sched_barrier(0);
-    return t;
-}
-#define TPT_STAMP(st, i)                          \
-    do {                                          \
-        const unsigned long long t_ = stamp_now(); \
-        (st).acc[i] += t_ - (st).last;            \
-        (st).last = t_;                           \
-    } while (0)
-#define TPT_STAMPS_ARG , Stamps& st
-#define TPT_STAMPS_PASS , st
-#else
-#define TPT_STAMP(st, i) \
-    do {                 \
-    } while (0)
-#define TPT_STAMPS_ARG
-#define TPT_STAMPS_PASS
-#endif
 // The camera hit and its material are invariant over a pixel's spp loop.  Held in
 // registers across the loop they cost ~25 VGPRs at every point of the sample body
 // and push the kernel into scratch spills; instead each lane parks them in LDS
@@ -1331,7 +942,7 @@ struct PixPark {
 // direct lighting from every emitter, then the unconditional `break` (:109).
 // The camera hit is the same for every sample of a pixel (no jitter,
 // SceneRenderingHelper.cpp:16-22): the caller computes it once and parks it in `px`.
-TPT_D V3 pt_sample(const DScene& s, PixPark px, uint32_t& rs, int* stk, Packet pk TPT_STAMPS_ARG) {
+TPT_D V3 pt_sample(const DScene& s, PixPark px, uint32_t& rs) {
     V3 result = v3s(0.0f);
     {
         const DMat& dm = s.mats[px.mat_index()];
@@ -1339,7 +950,6 @@ TPT_D V3 pt_sample(const DScene& s, PixPark px, uint32_t& rs, int* stk, Packet p
     }
     float pdf_b;
     V3 wib = mat_sample(px.mat(), px.v(kPxWo), px.shade(), &pdf_b, rs);
-    TPT_STAMP(st, 1);
     for (int li = 0; li < s.n_emitters; ++li) {
         const DObj o = s.objs[s.emitters[li]];
         // DirectLightSampler::sample (PathTracer.cpp:26-40)
@@ -1352,14 +962,12 @@ TPT_D V3 pt_sample(const DScene& s, PixPark px, uint32_t& rs, int* stk, Packet p
         float ct = (float)dot3(pn, -wil);
         float pll = (float)((double)o.pdf * d2 / (double)fabs_(ct));
         V3 ev = v3s(0.0f);
-        TPT_STAMP(st, 2);
         {
             // DirectLightSampler::pdf (PathTracer.cpp:14-24) on the BSDF direction
             const V3 hx0 = px.v(kPxX);
             Ray rb = make_ray(hx0, wib);
             Hit hnc, hb;
-            object_hit_nocull_back(s, o, rb, hnc, hb, stk);
-            TPT_STAMP(st, 3);
+            object_hit_nocull_back(s, o, rb, hnc, hb);
             float pbl = 0.0f;
             if (hnc.prim >= 0) {
                 V3 hx, hn;
@@ -1372,29 +980,22 @@ TPT_D V3 pt_sample(const DScene& s, PixPark px, uint32_t& rs, int* stk, Packet p
                 if (hb.prim >= 0) {
                     V3 hx, hn;
                     hit_geometry(s, rb, hb, hx, hn);
-                    TPT_STAMP(st, 4);
-                    const bool sh = shadow_q_packet(s, hx, px.v(kPxX), TPT_CULL_BACK, pk);
-                    TPT_STAMP(st, 5);
+                    const bool sh = shadow_ray(s, hx, px.v(kPxX), TPT_CULL_BACK);
                     if (!sh)
                         ev = ev + divs(eval_bsdf(px.mat(), px.v(kPxWo), wib, px.shade(), true), 1e-4f + pdf_b + pbl);
-                    TPT_STAMP(st, 6);
                 }
             }
         }
         // the light branch (PathTracer.cpp:95-106); plb is pure, so it is computed here
         float plb = mat_pdf(px.mat(), px.v(kPxWo), px.shade(), wil);
-        TPT_STAMP(st, 7);
         if (pll + plb > 0.0f) {
             Ray rl = make_ray(px.v(kPxX), wil);
-            Hit hl = object_hit(s, o, rl, TPT_CULL_BACK, stk);
+            Hit hl = object_hit(s, o, rl, TPT_CULL_BACK);
             V3 hx = v3s(0.0f), hn;  // default Intersection::coords when missed (Intersection.hpp:14-21)
             if (hl.prim >= 0) hit_geometry(s, rl, hl, hx, hn);
-            TPT_STAMP(st, 8);
-            const bool sh = shadow_q_packet(s, hx, px.v(kPxX), TPT_CULL_BACK, pk);
-            TPT_STAMP(st, 9);
+            const bool sh = shadow_ray(s, hx, px.v(kPxX), TPT_CULL_BACK);
             if (!sh)
                 ev = ev + divs(eval_bsdf(px.mat(), px.v(kPxWo), wil, px.shade(), true), 1e-4f + pll + plb);
-            TPT_STAMP(st, 10);
         }
         result = result + ev * load_mat(s, o.mat).em;
     }
@@ -1415,7 +1016,7 @@ struct PtiPath {
     int nb;     // outBounces
     bool flip;  // lastBounceFlipCulling
 };
-TPT_D bool pti_step(const DScene& s, const PTV& v, PtiPath& p, uint32_t& rs, int* stk, Packet pk) {
+TPT_D bool pti_step(const DScene& s, const PTV& v, PtiPath& p, uint32_t& rs) {
     const int mi = prim_mat(s, v.prim);
     const Mat m = load_mat(s, mi);
     if (p.nb == 0 && s.mats[mi].has_em) p.res = p.res + p.alpha * m.em;  // :64-68
@@ -1437,7 +1038,7 @@ TPT_D bool pti_step(const DScene& s, const PTV& v, PtiPath& p, uint32_t& rs, int
         {
             const Ray rb = make_ray(x, wib);
             Hit hnc, hb;
-            object_hit_nocull_back(s, o, rb, hnc, hb, stk);
+            object_hit_nocull_back(s, o, rb, hnc, hb);
             float pbl = 0.0f;
             if (hnc.prim >= 0) {
                 V3 hx, hn;
@@ -1449,17 +1050,17 @@ TPT_D bool pti_step(const DScene& s, const PTV& v, PtiPath& p, uint32_t& rs, int
             if (pdf_b + pbl > 0.0f && hb.prim >= 0) {
                 V3 hx, hn;
                 hit_geometry(s, rb, hb, hx, hn);
-                if (!shadow_q_packet(s, hx, x, TPT_CULL_BACK, pk))
+                if (!shadow_ray(s, hx, x, TPT_CULL_BACK))
                     ev = ev + divs(eval_bsdf(m, wo, wib, sh, true), 1e-4f + pdf_b + pbl);
             }
         }
         const float plb = mat_pdf(m, wo, sh, wil);
         if (pll + plb > 0.0f) {
             const Ray rl = make_ray(x, wil);
-            const Hit hl = object_hit(s, o, rl, TPT_CULL_BACK, stk);
+            const Hit hl = object_hit(s, o, rl, TPT_CULL_BACK);
             V3 hx = v3s(0.0f), hn;  // default Intersection::coords when missed
             if (hl.prim >= 0) hit_geometry(s, rl, hl, hx, hn);
-            if (!shadow_q_packet(s, hx, x, TPT_CULL_BACK, pk))
+            if (!shadow_ray(s, hx, x, TPT_CULL_BACK))
                 ev = ev + divs(eval_bsdf(m, wo, wil, sh, true), 1e-4f + pll + plb);
         }
         p.res = p.res + p.alpha * ev * load_mat(s, o.mat).em;  // :105

@@ -45,17 +45,6 @@ static const int32_t kMeshExit = -2;
 // (tpt_scene_build.cpp: split_walk_groups).
 static const int kFlatMaxLeaves = 64;
 
-// 128 B: a 4-wide node for shadow (any-hit) queries, made by collapsing two levels
-// of the binary tree (tpt_scene_build.cpp: build_qnodes).  Child j's box is the
-// binary node's own box; child >= 0 is another DQNode, child < 0 a leaf as in
-// DNode::a, kEmptyLeaf an unused slot (its box is inverted and never overlaps).
-struct DQNode {
-    float bmin[3][4];  // [axis][child]
-    float bmax[3][4];
-    int32_t child[4];
-    int32_t pad[4];
-};
-
 // 48 B, read as three float4: (v0, n.x) (e1, n.y) (e2, n.z) -- Triangle.hpp:46-50
 struct DTri {
     float v0[3];
@@ -112,7 +101,6 @@ struct DScene {
     const DMat* mats;
     const DObj* objs;
     const int32_t* emitters;  // Scene::m_emissionObjects (object ids)
-    const DQNode* qnodes;     // 4-wide shadow tree, root at 0
     const DNode* tnodes;      // threaded binary tree (stackless walks), same indices as nodes
     const DNode* leaves;      // primitive leaves in the reference's DFS order (flat queries)
     const DNode* groups;      // leaves grouped per object: box, a = first leaf, b = count;
@@ -120,7 +108,7 @@ struct DScene {
     const DTri* ftris;        // triangle of flat leaf j is ftris[leaves[j].b]
     int32_t nleaf;
     int32_t ngroup;
-    int32_t flat;             // flat (all-leaves) queries: kFlatShadow | kFlatHit | kFlatPkShadow bits, 0 = tree walks
+    int32_t flat;             // flat (all-leaves) queries: kFlatShadow | kFlatHit bits, 0 = tree walks
     int32_t n_emitters;
     int32_t light_draws;  // XorShift draws of one DirectLightSampler::sample pass over all emitters
     int32_t ntri;
@@ -132,14 +120,9 @@ struct DScene {
     float scale;  // CalculateScale(fov) (SceneRenderingHelper.cpp:12-14), host-computed
     float eye[3];
     float bg[3];
-    int32_t nqnodes;
     int32_t nmats;
-    int32_t max_stack;  // LDS stack entries per lane a binary-tree walk can need (depth + 1)
-    int32_t q_stack;    // ... and a per-lane walk of the 4-wide shadow tree (3 per level + 1)
     int32_t lds_bytes;  // bytes staged in LDS per workgroup (0 = read from HBM/L2)
-    int32_t lds_full;   // 1: nodes + triangles + qnodes + flat arrays staged; 0: only the flat arrays
-    int32_t dbg;        // ablation switches for profiling only (TPT_DEBUG_FLAGS); 0 in production
-    unsigned long long* dbgc;  // profiling counters (TPT_DEBUG_FLAGS & 2)
+    int32_t lds_full;   // 1: nodes + triangles + flat arrays staged; 0: only the flat arrays
 };
 
 }  // namespace tpt

@@ -116,59 +116,6 @@ DNode to_dnode(const Box& b, int a, int c) {
 
 }  // namespace
 
-// Collapse two levels of the binary tree into one 4-wide node (children of the
-// children; a leaf child is kept as is).  Exactness for shadow queries: a parent
-// box is the exact componentwise min/max of its children's boxes, and the slab
-// test (Bounds3::IntersectP) is monotone in the box bounds -- fl(b - o) and
-// fl(x * inv) are monotone in b, std::max/std::min preserve order, and a NaN slab
-// (0 * inf) only arises where the bigger box yields an unconstrained slab too -- so
-// a binary node's box passing implies every ancestor box passes.  The set of
-// primitives the reference tests for a ray is therefore exactly the set whose leaf
-// box passes, whichever intermediate boxes are skipped, and an any-hit query over
-// that set is order-independent.  Returns the depth of the 4-wide tree.
-static int build_q(HostScene& hs, int bi) {
-    const int q = (int)hs.qnodes.size();
-    hs.qnodes.push_back(DQNode{});
-    int entry[4], ne = 0;
-    const DNode& n = hs.nodes[bi];
-    if (n.a < 0) {
-        entry[ne++] = bi;  // a leaf root
-    } else {
-        for (int c : {n.a, n.b}) {
-            const DNode& cn = hs.nodes[c];
-            if (cn.a >= 0) { entry[ne++] = cn.a; entry[ne++] = cn.b; }
-            else entry[ne++] = c;
-        }
-    }
-    int child[4], depth = 1;
-    for (int j = 0; j < ne; ++j) {
-        const DNode& e = hs.nodes[entry[j]];
-        if (e.a >= 0) {
-            const int d = build_q(hs, entry[j]);
-            child[j] = d >> 8;
-            depth = std::max(depth, (d & 0xff) + 1);
-        } else {
-            child[j] = e.a;  // -1 - prim or kEmptyLeaf
-        }
-    }
-    DQNode& Q = hs.qnodes[q];
-    for (int j = 0; j < 4; ++j) {
-        const bool used = j < ne && child[j] != kEmptyLeaf;
-        for (int ax = 0; ax < 3; ++ax) {
-            Q.bmin[ax][j] = used ? hs.nodes[entry[j]].bmin[ax] : 3.40282347e+38f;
-            Q.bmax[ax][j] = used ? hs.nodes[entry[j]].bmax[ax] : -3.40282347e+38f;
-        }
-        Q.child[j] = used ? child[j] : kEmptyLeaf;
-    }
-    return (q << 8) | std::min(depth, 255);
-}
-
-static int build_qnodes(HostScene& hs) {
-    hs.qnodes.clear();
-    if (hs.nodes.empty()) return 0;
-    return build_q(hs, 0) & 0xff;
-}
-
 // Threading (tpt_scene.h, tnodes): node n's miss link is the node the reference's
 // DFS pops after n's subtree.  Scene-level nodes [0, ntop) are threaded as one
 // tree whose spliced mesh leaves keep their next link and point into the mesh;
@@ -435,17 +382,11 @@ int build_host_scene(const tpt_scene_desc* d, HostScene& hs, std::string& err) {
             hs.node_area[gi] = n.area;
         }
     }
-    int max_depth = 0;
-    // depth of the spliced tree: scene-level depth of the leaf + mesh depth - 1
-    std::vector<int> top_level(ntop, 1);
     for (int k = 0; k < ntop; ++k) {
         const BuildNode& n = top.nodes[k];
         if (n.item < 0) {
-            top_level[n.left] = top_level[k] + 1;
-            top_level[n.right] = top_level[k] + 1;
             hs.nodes[k] = to_dnode(n.box, n.left, n.right);
             hs.node_area[k] = n.area;
-            max_depth = std::max(max_depth, top_level[k]);
             continue;
         }
         int o = n.item;
@@ -455,18 +396,11 @@ int build_host_scene(const tpt_scene_desc* d, HostScene& hs, std::string& err) {
                 DNode root = hs.nodes[mesh_base[o]];
                 hs.nodes[k] = to_dnode(n.box, root.a, root.b);  // identical box, see tpt_scene.h
             }
-            max_depth = std::max(max_depth, top_level[k] + std::max(mtree[o].depth, 1) - 1);
         } else {
             hs.nodes[k] = to_dnode(n.box, -1 - sphere_prim[o], -1);
-            max_depth = std::max(max_depth, top_level[k]);
         }
         hs.node_area[k] = n.area;
     }
-    for (int o = 0; o < d->num_objects; ++o) max_depth = std::max(max_depth, mtree[o].depth);
-    // The reference's push-two stack (BVH.cpp:121-140) holds at most depth+1 entries.
-    hs.max_stack = max_depth + 1;
-    // The 4-wide shadow tree pushes at most 3 entries per level of ceil(depth/2) levels.
-    hs.q_stack = 3 * build_qnodes(hs) + 1;
     build_threads(hs, ntop, mesh_base);
 
     // ---- objects and emitters

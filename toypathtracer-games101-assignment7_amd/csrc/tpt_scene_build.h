@@ -10,7 +10,6 @@ namespace tpt {
 
 struct HostScene {
     std::vector<DNode> nodes;
-    std::vector<DQNode> qnodes;
     std::vector<DNode> tnodes;
     std::vector<DNode> leaves;  // primitive leaves in the reference's visit order (flat queries)
     std::vector<DNode> groups;  // per object: its box, first leaf (a) and leaf count (b); b < 0: walk group
@@ -27,8 +26,6 @@ struct HostScene {
     float eye[3] = {0, 0, 0};
     float bg[3] = {0, 0, 0};
     double fov = 40.0;
-    int max_stack = 1;
-    int q_stack = 1;
 };
 
 int build_host_scene(const tpt_scene_desc* d, HostScene& hs, std::string& err);
