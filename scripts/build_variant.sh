@@ -8,9 +8,9 @@ root=$(cd "$(dirname "$0")/.." && pwd)
 pkg=$root/toypathtracer-games101-assignment7_amd
 out=$root/variants/$name
 mkdir -p "$out"
-make -s -C "$pkg" build/tpt_scene_build.o build/scene_api.o build/film.o
+make -s -C "$pkg" build/tpt_scene_build.o build/tpt_multi.o build/scene_api.o build/film.o
 /opt/rocm/bin/hipcc -std=c++17 -O3 -fPIC -ffp-contract=off -Wno-unused-function --offload-arch=gfx950 \
     -munsafe-fp-atomics "$@" -c -o "$out/tpt_capi.o" "$pkg/csrc/tpt_capi.hip"
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o "$out/libtpt.so" "$out/tpt_capi.o" \
-    "$pkg/build/tpt_scene_build.o" "$pkg/build/scene_api.o" "$pkg/build/film.o"
+    "$pkg/build/tpt_scene_build.o" "$pkg/build/tpt_multi.o" "$pkg/build/scene_api.o" "$pkg/build/film.o" -ldl
 echo "built $out/libtpt.so ($*)"
