@@ -105,53 +105,68 @@ TPT_D uint32_t skip_samples(uint32_t st, int type, int light_draws, int n) {
     return st;
 }
 
+#ifndef TPT_PT_LANES
+#define TPT_PT_LANES 8  // Q lanes per PT pixel stream (1, 2, 4, 8 or 16; 8 measured best on one MI355X)
+#endif
+constexpr int kQ = TPT_PT_LANES;
+static_assert(kQ == 1 || kQ == 2 || kQ == 4 || kQ == 8 || kQ == 16, "Q must be a power of two dividing the wave");
+
 template <bool kLds>
 __global__ __launch_bounds__(kBlock, TPT_PT_MINWAVES) void tpt_pt_kernel(DScene s, int spp, int64_t begin,
                                                                         int64_t stride, int64_t count,
                                                                         const int64_t* __restrict__ list,
-                                                                        float* __restrict__ out, int Q) {
+                                                                        float* __restrict__ out) {
     unsigned char* lds_free = stage_scene<kLds>(s);
-    const int64_t gl = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    const int64_t k = gl / Q;      // pixel ordinal in the shard / list
-    const int q = (int)(gl % Q);   // this lane's sample phase
-    const bool on = k < count;
-    const int64_t i = on ? (list ? list[k] : begin + k * stride) : 0;
-    const int64_t row = list ? k : i;
-    const int px = (int)(i % s.width), py = (int)(i / s.width);
-    const V3 dir = pixel_ray(px, py, s.width, s.height, s.scale);
-    const Ray r = make_ray(v3(s.eye[0], s.eye[1], s.eye[2]), dir);
-    PTV v = scene_intersect(s, r, TPT_CULL_BACK);
-    const bool hit = on && v.type != T_BG;
     V3 acc = v3s(0.0f);
-    if (hit) {
-        const int mi = prim_mat(s, v.prim);
-        const Mat m = load_mat(s, mi);
-        PixPark px;
-        px.base = reinterpret_cast<float*>(lds_free);
-        px.park(v.x, v.N, -dir, mi, m);
-        const float inv = 1.0f / spp;
-        uint32_t rs = (uint32_t)((int)i + 1);  // ResetRandom(i + 1), Renderer.cpp:42
-        rs = skip_samples(rs, m.type, s.light_draws, q);
-        const int base = lane_id() - q;       // first lane of this pixel (Q divides 64)
-        for (int j0 = 0; j0 < spp; j0 += Q) {
-            V3 L = v3s(0.0f);
-            if (j0 + q < spp) {
-                L = mul(pt_sample(s, px, rs), inv);
-                if (Q > 1) rs = skip_samples(rs, m.type, s.light_draws, Q - 1);
-            }
-            if (Q == 1) {
-                acc = acc + L;
-            } else {
-                const int n = spp - j0 < Q ? spp - j0 : Q;
-                for (int jj = 0; jj < n; ++jj) {
-                    acc.x = acc.x + __shfl(L.x, base + jj);
-                    acc.y = acc.y + __shfl(L.y, base + jj);
-                    acc.z = acc.z + __shfl(L.z, base + jj);
+    {
+        const int64_t gl = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+        const int64_t k = gl / kQ;  // pixel ordinal in the shard / list
+        const int q = (int)(gl % kQ);  // this lane's sample phase
+        const bool on = k < count;
+        const int64_t i = on ? (list ? list[k] : begin + k * stride) : 0;
+        const int px = (int)(i % s.width), py = (int)(i / s.width);
+        const V3 dir = pixel_ray(px, py, s.width, s.height, s.scale);
+        const Ray r = make_ray(v3(s.eye[0], s.eye[1], s.eye[2]), dir);
+        PTV v = scene_intersect(s, r, TPT_CULL_BACK);
+        if (on && v.type != T_BG) {
+            const int mi = prim_mat(s, v.prim);
+            const Mat m = load_mat(s, mi);
+            PixPark px;
+            px.base = reinterpret_cast<float*>(lds_free);
+            px.park(v.x, v.N, -dir, mi, m);
+            const float inv = 1.0f / spp;
+            uint32_t rs = (uint32_t)((int)i + 1);  // ResetRandom(i + 1), Renderer.cpp:42
+            rs = skip_samples(rs, m.type, s.light_draws, q);
+            // Only acc, rs and the loop counter stay live across the sample loop: the
+            // lane's phase, the material type (parked) and the output row are
+            // recomputed where they are used, so nothing spills around the loop.
+            for (int j0 = 0; j0 < spp; j0 += kQ) {
+                const int qq = lane_id() & (kQ - 1);  // == q: blocks hold whole pixels
+                V3 L = v3s(0.0f);
+                if (j0 + qq < spp) {
+                    L = mul(pt_sample(s, px, rs), inv);
+                    if (kQ > 1) rs = skip_samples(rs, px.type(), s.light_draws, kQ - 1);
+                }
+                if (kQ == 1) {
+                    acc = acc + L;
+                } else {
+                    const int base = lane_id() - qq;  // first lane of this pixel
+                    const int n = spp - j0 < kQ ? spp - j0 : kQ;
+                    for (int jj = 0; jj < n; ++jj) {
+                        acc.x = acc.x + __shfl(L.x, base + jj);
+                        acc.y = acc.y + __shfl(L.y, base + jj);
+                        acc.z = acc.z + __shfl(L.z, base + jj);
+                    }
                 }
             }
         }
     }
-    if (on && q == 0) {
+    unsigned tid = threadIdx.x;
+    asm volatile("" : "+v"(tid));  // recomputed, not kept alive across the loop
+    const int64_t gl = (int64_t)blockIdx.x * kBlock + tid;
+    const int64_t k = gl / kQ;
+    if (k < count && gl % kQ == 0) {
+        const int64_t row = list ? k : begin + k * stride;
         out[3 * row + 0] = acc.x;
         out[3 * row + 1] = acc.y;
         out[3 * row + 2] = acc.z;
@@ -451,14 +466,9 @@ __global__ __launch_bounds__(kBlock) void tpt_intersect_kernel(DScene s, const f
 }
 
 // ------------------------------------------------------------------ C ABI --
-#ifndef TPT_PT_LANES
-#define TPT_PT_LANES 8  // Q lanes per PT pixel stream (1, 2, 4, 8 or 16; 8 measured best on one MI355X)
-#endif
 #ifndef TPT_BDPT_SERIAL
 #define TPT_BDPT_SERIAL 0  // 1: connect / fold on the gen stream (per-kernel timing builds only)
 #endif
-static_assert(TPT_PT_LANES == 1 || TPT_PT_LANES == 2 || TPT_PT_LANES == 4 || TPT_PT_LANES == 8 || TPT_PT_LANES == 16,
-              "Q must divide the wave");
 
 struct tpt_ctx {
     int device = 0;
@@ -479,7 +489,6 @@ struct tpt_ctx {
     unsigned long long* counters = nullptr;
     unsigned* queue = nullptr;  // persistent gen: 8 shard counters, 64 B apart
     int num_cu = 0;
-    int pt_lanes = TPT_PT_LANES;  // Q: lanes per pixel of the PT kernel
     // wavefront BDPT state (sized for wf_cap pixels)
     void* wf_mem = nullptr;
     int64_t wf_cap = 0;
@@ -589,15 +598,14 @@ int launch(tpt_ctx* c, int mode, int spp, int64_t begin, int64_t stride, int64_t
     const bool lds = c->ds.lds_bytes > 0;
     const size_t shmem = (size_t)c->ds.lds_bytes;
     if (mode == TPT_MODE_PT) {
-        const int Q = c->pt_lanes;
-        const int64_t qblocks = (count * Q + kBlock - 1) / kBlock;
+        const int64_t qblocks = (count * kQ + kBlock - 1) / kBlock;
         const size_t pshmem = shmem + (size_t)kPixSlots * kBlock * sizeof(float);
         if (lds)
             hipLaunchKernelGGL(tpt_pt_kernel<true>, dim3((unsigned)qblocks), dim3(kBlock), pshmem, c->stream, c->ds,
-                               spp, begin, stride, count, dlist, drows, Q);
+                               spp, begin, stride, count, dlist, drows);
         else
             hipLaunchKernelGGL(tpt_pt_kernel<false>, dim3((unsigned)qblocks), dim3(kBlock), pshmem, c->stream, c->ds,
-                               spp, begin, stride, count, dlist, drows, Q);
+                               spp, begin, stride, count, dlist, drows);
     } else if (mode == TPT_MODE_PT_INDIRECT) {
         if (lds)
             hipLaunchKernelGGL(tpt_pti_kernel<true>, dim3((unsigned)blocks), dim3(kBlock), shmem, c->stream, c->ds, spp,

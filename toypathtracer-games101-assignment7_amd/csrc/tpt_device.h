@@ -895,6 +895,7 @@ struct PixPark {
         return v3(p[k * kBlock], p[(k + 1) * kBlock], p[(k + 2) * kBlock]);
     }
     TPT_D int mat_index() const { return __float_as_int(lane()[kPxMat * kBlock]); }
+    TPT_D int type() const { return __float_as_int(lane()[kPxType * kBlock]); }
     TPT_D Shade shade() const {
         Shade f;
         f.n = v(kPxN);
