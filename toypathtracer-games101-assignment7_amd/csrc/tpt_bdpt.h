@@ -288,7 +288,7 @@ TPT_D void camera_vertices(const DScene& s, int64_t i, BVert& c0, BVert& c1) {
 //   scan:    inclusive prefix sums of the strategy counts (s = 0 ones and the others);
 //   scatter: task[g] = (pixel, t, s) for every strategy, the s = 0 (emission-only)
 //            strategies first and the connecting ones after, so a wave holds one
-//            kind; tres[g] = the strategy's canonical (t, s)-order slot;
+//            kind (4 B per task; the result slot is the task's own index);
 //   connect: ONE LANE PER STRATEGY (PathWeight), so a wave's work is 64 strategies
 //            instead of the longest lane's cn*(ln+1) (measured 18 mean vs 73 max);
 //            t = 1 splats go straight to the splat buffer;
@@ -307,15 +307,20 @@ struct WfState {
     unsigned long long* incl;   // inclusive scan of np (both halves at once)
     unsigned long long* np2;
     unsigned long long* incl2;  // inclusive scan of np2
-    int* tres;            // task -> canonical strategy index (res slot)
-    unsigned long long* task;  // strategy -> pixel | t << 40 | s << 48
-    float* res;           // 3 floats per strategy
+    unsigned* task;       // strategy -> pixel | t << 22 | s << 27 (pixel < kWfChunk)
+    float* res;           // 3 floats per strategy, in task order
     uint32_t* rng;        // XorShift state per pixel stream
     float* acc;           // 3 floats per pixel
     const int64_t* list;  // pixel list (or null: begin + k*stride)
     int64_t begin, stride, n;
     unsigned long long* bounces;
 };
+// One wavefront holds at most kWfChunk pixel streams (launch() splits larger shards):
+// the task record keeps the pixel in 22 bits and the per-class scans count in 32.
+constexpr int64_t kWfChunk = int64_t(1) << 22;
+constexpr unsigned kTaskPixelMask = (unsigned)kWfChunk - 1;
+static_assert(kMaxLen < 32, "task records keep t and s in 5 bits each");
+static_assert(kWfChunk * (kMaxLen * (kMaxLen + 1)) < (int64_t(1) << 32), "per-class scan halves are 32-bit");
 TPT_D int64_t wf_pixel(const WfState& w, int64_t k) { return w.list ? w.list[k] : w.begin + k * w.stride; }
 TPT_D int tp_pack(int type, int prim) { return (prim + 1) * 4 + type; }
 TPT_D float4* rec_at(float4* rec, int64_t k, int slot) { return rec + ((k * (2 * kMaxLen) + slot) * kRecV); }

@@ -338,7 +338,6 @@ __global__ __launch_bounds__(kBlock, TPT_GEN_MINWAVES) void tpt_bdpt_gen_kernel(
 // so a wave's 64 strategies are (nearly always) of one class and take the same
 // branches through PathWeight.  Results still land in their canonical (t, s) slots.
 struct StratRange {
-    int64_t canon;       // first canonical slot of the pixel
     int64_t b[4];        // the pixel's start in each run (absolute task index)
     int ln, np;          // light vertices, strategies
 };
@@ -351,7 +350,6 @@ TPT_D StratRange strat_range(const WfState& w, int64_t k) {
     const int64_t xD = (int64_t)(e2 & 0xffffffffull) - (int64_t)(c2 & 0xffffffffull);
     const int64_t xT = (int64_t)(e2 >> 32) - (int64_t)(c2 >> 32);
     StratRange r;
-    r.canon = xA + xE + xD + xT;
     r.b[0] = xA;
     r.b[1] = totA + xE;
     r.b[2] = totA + totE + xD;
@@ -378,8 +376,7 @@ __global__ __launch_bounds__(kBlock) void tpt_bdpt_scatter_kernel(WfState w, uns
         else if (t == 1) g = r.b[3] + (sl - 1);
         else if (sl == 1) g = r.b[2] + (t - 2);
         else g = r.b[1] + (int64_t)(t - 2) * (ln - 1) + (sl - 2);
-        w.task[g] = (unsigned long long)k | ((unsigned long long)t << 40) | ((unsigned long long)sl << 48);
-        w.tres[g] = (int)(r.canon + pi - 1);
+        w.task[g] = (unsigned)k | (unsigned)t << 22 | (unsigned)sl << 27;
     }
 }
 
@@ -396,17 +393,17 @@ __global__ __launch_bounds__(kBlock, TPT_CONN_MINWAVES) void tpt_bdpt_conn_kerne
         V3 v = v3s(0.0f), lx = eye;
         bool sp = false;
         if (g < total) {
-            const unsigned long long tk = w.task[g];
-            const int64_t k = (int64_t)(tk & 0xffffffffffull);
-            const int t = (int)((tk >> 40) & 0xff), sl = (int)(tk >> 48);
+            const unsigned tk = w.task[g];
+            const int64_t k = (int64_t)(tk & kTaskPixelMask);
+            const int t = (int)((tk >> 22) & 31), sl = (int)(tk >> 27);
             GlobPaths P;
             P.rec = rec_at(w.rec, k, 0);
             v = vmax0(path_weight(s, P, sl, t));
-            if (t > 1) {
-                const int64_t ri = w.tres[g];
-                w.res[3 * ri] = v.x;
-                w.res[3 * ri + 1] = v.y;
-                w.res[3 * ri + 2] = v.z;
+            if (t > 1) {  // the result stays in task order; fold finds it from (t, s)
+                const int64_t gr = g;
+                w.res[3 * gr] = v.x;
+                w.res[3 * gr + 1] = v.y;
+                w.res[3 * gr + 2] = v.z;
             } else if (splat) {
                 sp = true;
                 lx = P.lit(sl - 1).x;
@@ -424,11 +421,17 @@ __global__ __launch_bounds__(kBlock) void tpt_bdpt_fold_kernel(WfState w, float 
     const int64_t k = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (k >= w.n) return;
     const StratRange r = strat_range(w, k);
-    const int64_t b = r.canon, e = r.canon + r.np;
-    const int ln = r.ln;
+    const int ln = r.ln, cn = w.cnt[k] & 0xffff;
     V3 res = v3s(0.0f);  // BDPT.cpp:289 `Vector3f result;`
-    for (int64_t g = b + ln; g < e; ++g)  // pi = g - b + 1 > ln: t > 1 (t = 1 strategies were splatted)
-        res = res + v3(w.res[3 * g], w.res[3 * g + 1], w.res[3 * g + 2]);
+    // the t > 1 strategies in (t, s) order (t = 1 ones were splatted), each read from
+    // its place in the task runs -- the same positions tpt_bdpt_scatter_kernel wrote
+    auto add = [&](int64_t g) { res = res + v3(w.res[3 * g], w.res[3 * g + 1], w.res[3 * g + 2]); };
+    for (int t = 2; t <= cn; ++t) {
+        add(r.b[0] + (t - 2));  // s = 0
+        add(r.b[2] + (t - 2));  // s = 1
+        const int64_t g1 = r.b[1] + (int64_t)(t - 2) * (ln - 1) - 2;
+        for (int sl = 2; sl <= ln; ++sl) add(g1 + sl);
+    }
     V3 acc = v3(w.acc[3 * k], w.acc[3 * k + 1], w.acc[3 * k + 2]);
     acc = acc + mul(res, inv);  // Renderer.cpp:49 `fb[i] += (1.0f / spp) * BDPT(...)`
     w.acc[3 * k] = acc.x;
@@ -550,8 +553,8 @@ int ensure_wf(tpt_ctx* c, int64_t n) {
     const int64_t maxs = (int64_t)kMaxLen * (kMaxLen + 1) - 1;
     auto al = [](int64_t b) { return (b + 255) & ~(int64_t)255; };
     const int64_t b_rec = al(2 * kMaxLen * kRecV * n * 16), b_i = al(n * 4), b_l = al(n * 8),
-                  b_own = al(n * maxs * 8), b_tres = al(n * maxs * 4), b_res = al(n * maxs * 12), b_acc = al(n * 12);
-    const int64_t per_buf = b_rec + b_i + 4 * b_l + b_own + b_tres + b_res;
+                  b_own = al(n * maxs * 4), b_res = al(n * maxs * 12), b_acc = al(n * 12);
+    const int64_t per_buf = b_rec + b_i + 4 * b_l + b_own + b_res;
     const int64_t total = 2 * per_buf + b_i + b_acc;
     HIP_TRY(c, hipMalloc(&c->wf_mem, total));
     char* p = (char*)c->wf_mem;
@@ -563,8 +566,7 @@ int ensure_wf(tpt_ctx* c, int64_t n) {
         w.incl = (unsigned long long*)p; p += b_l;
         w.np2 = (unsigned long long*)p; p += b_l;
         w.incl2 = (unsigned long long*)p; p += b_l;
-        w.task = (unsigned long long*)p; p += b_own;
-        w.tres = (int*)p; p += b_tres;
+        w.task = (unsigned*)p; p += b_own;
         w.res = (float*)p; p += b_res;
     }
     c->wf[0].rng = c->wf[1].rng = (uint32_t*)p; p += b_i;
@@ -582,6 +584,76 @@ int ensure_wf(tpt_ctx* c, int64_t n) {
 int64_t shard_count(int64_t npix, int64_t begin, int64_t stride) {
     if (begin >= npix) return 0;
     return (npix - begin + stride - 1) / stride;
+}
+
+// One BDPT wavefront over `count` (<= kWfChunk) pixel streams.
+int launch_bdpt_chunk(tpt_ctx* c, int spp, int64_t begin, int64_t stride, int64_t count, const int64_t* dlist,
+                      float* drows, float* dsplat) {
+    const bool lds = c->ds.lds_bytes > 0;
+    const size_t shmem = (size_t)c->ds.lds_bytes;
+    // Two streams: gen/scan/scatter of iteration it on c->stream, connect/fold on
+    // c->stream2, with the wavefront state double-buffered so gen(it+1) runs
+    // beside connect(it) and fills the tail of each.  Ordering per pixel is kept:
+    // gen is sequential on one stream (RNG state), fold is sequential on the other
+    // (acc, splat), and buffer b is rewritten by gen(it+2) only after fold(it).
+    hipStream_t s2 = TPT_BDPT_SERIAL ? c->stream : c->stream2;
+    HIP_TRY(c, hipEventRecord(c->ev_fold[0], c->stream));
+    HIP_TRY(c, hipStreamWaitEvent(s2, c->ev_fold[0], 0));  // stream2 starts after ev0
+    const unsigned pblocks = (unsigned)((count + kBlock - 1) / kBlock);
+    const unsigned cblocks = (unsigned)std::min<int64_t>(8192, (count * 24 + kBlock - 1) / kBlock + 1);
+    // persistent gen grid: as many workgroups as are resident at once, a multiple of
+    // the 8 queue shards, and no more than the pixels need
+    int per_cu = 0;
+    HIP_TRY(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                   &per_cu, lds ? (const void*)tpt_bdpt_gen_kernel<true> : (const void*)tpt_bdpt_gen_kernel<false>,
+                   kBlock, shmem));
+    int64_t gb = (int64_t)std::max(per_cu, 1) * std::max(c->num_cu, 1);
+    gb = std::min<int64_t>(gb, ((int64_t)pblocks + 7) / 8 * 8);
+    const unsigned gblocks = (unsigned)std::max<int64_t>(8, gb / 8 * 8);
+    const float inv = 1.0f / spp;
+    for (int it = 0; it < spp; ++it) {
+        const int b = it & 1;
+        WfState w = c->wf[b];
+        w.list = dlist;
+        w.begin = begin;
+        w.stride = stride;
+        w.n = count;
+        w.bounces = c->counters;
+        if (it >= 2) HIP_TRY(c, hipStreamWaitEvent(c->stream, c->ev_fold[b], 0));
+        if (it == 0) HIP_TRY(c, hipMemsetAsync(c->queue, 0, 8 * 64, c->stream));  // later: reset by scatter
+        if (lds)
+            hipLaunchKernelGGL(tpt_bdpt_gen_kernel<true>, dim3(gblocks), dim3(kBlock), shmem, c->stream, c->ds, w, it,
+                               c->queue);
+        else
+            hipLaunchKernelGGL(tpt_bdpt_gen_kernel<false>, dim3(gblocks), dim3(kBlock), shmem, c->stream, c->ds, w, it,
+                               c->queue);
+        size_t bytes = c->scan_bytes;
+        HIP_TRY(c, rocprim::inclusive_scan(c->scan_tmp, bytes, w.np, w.incl, (size_t)count,
+                                           rocprim::plus<unsigned long long>(),
+                                           c->stream));
+        bytes = c->scan_bytes;
+        HIP_TRY(c, rocprim::inclusive_scan(c->scan_tmp, bytes, w.np2, w.incl2, (size_t)count,
+                                           rocprim::plus<unsigned long long>(), c->stream));
+        hipLaunchKernelGGL(tpt_bdpt_scatter_kernel, dim3(pblocks), dim3(kBlock), 0, c->stream, w, c->queue);
+        HIP_TRY(c, hipEventRecord(c->ev_gen[b], c->stream));
+        HIP_TRY(c, hipStreamWaitEvent(s2, c->ev_gen[b], 0));
+        if (lds)
+            hipLaunchKernelGGL(tpt_bdpt_conn_kernel<true>, dim3(cblocks), dim3(kBlock), shmem, s2, c->ds, w,
+                               dsplat);
+        else
+            hipLaunchKernelGGL(tpt_bdpt_conn_kernel<false>, dim3(cblocks), dim3(kBlock), shmem, s2, c->ds,
+                               w, dsplat);
+        hipLaunchKernelGGL(tpt_bdpt_fold_kernel, dim3(pblocks), dim3(kBlock), 0, s2, w, inv);
+        HIP_TRY(c, hipEventRecord(c->ev_fold[b], s2));
+    }
+    HIP_TRY(c, hipStreamWaitEvent(c->stream, c->ev_fold[(spp - 1) & 1], 0));
+    WfState w = c->wf[0];
+    w.list = dlist;
+    w.begin = begin;
+    w.stride = stride;
+    w.n = count;
+    hipLaunchKernelGGL(tpt_bdpt_out_kernel, dim3(pblocks), dim3(kBlock), 0, c->stream, w, drows, dlist ? 1 : 0);
+    return TPT_OK;
 }
 
 // Launch the integration kernel for `count` pixels; rows/splat are device buffers.
@@ -614,70 +686,14 @@ int launch(tpt_ctx* c, int mode, int spp, int64_t begin, int64_t stride, int64_t
             hipLaunchKernelGGL(tpt_pti_kernel<false>, dim3((unsigned)blocks), dim3(kBlock), shmem, c->stream, c->ds,
                                spp, begin, stride, count, dlist, drows, c->counters);
     } else {
-        int rc = ensure_wf(c, count);
+        // Shards larger than kWfChunk pixel streams run as consecutive wavefronts.
+        int rc = ensure_wf(c, std::min(count, kWfChunk));
         if (rc) return rc;
-        // Two streams: gen/scan/scatter of iteration it on c->stream, connect/fold on
-        // c->stream2, with the wavefront state double-buffered so gen(it+1) runs
-        // beside connect(it) and fills the tail of each.  Ordering per pixel is kept:
-        // gen is sequential on one stream (RNG state), fold is sequential on the other
-        // (acc, splat), and buffer b is rewritten by gen(it+2) only after fold(it).
-        hipStream_t s2 = TPT_BDPT_SERIAL ? c->stream : c->stream2;
-        HIP_TRY(c, hipEventRecord(c->ev_fold[0], c->stream));
-        HIP_TRY(c, hipStreamWaitEvent(s2, c->ev_fold[0], 0));  // stream2 starts after ev0
-        const unsigned pblocks = (unsigned)((count + kBlock - 1) / kBlock);
-        const unsigned cblocks = (unsigned)std::min<int64_t>(8192, (count * 24 + kBlock - 1) / kBlock + 1);
-        // persistent gen grid: as many workgroups as are resident at once, a multiple of
-        // the 8 queue shards, and no more than the pixels need
-        int per_cu = 0;
-        HIP_TRY(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                       &per_cu, lds ? (const void*)tpt_bdpt_gen_kernel<true> : (const void*)tpt_bdpt_gen_kernel<false>,
-                       kBlock, shmem));
-        int64_t gb = (int64_t)std::max(per_cu, 1) * std::max(c->num_cu, 1);
-        gb = std::min<int64_t>(gb, ((int64_t)pblocks + 7) / 8 * 8);
-        const unsigned gblocks = (unsigned)std::max<int64_t>(8, gb / 8 * 8);
-        const float inv = 1.0f / spp;
-        for (int it = 0; it < spp; ++it) {
-            const int b = it & 1;
-            WfState w = c->wf[b];
-            w.list = dlist;
-            w.begin = begin;
-            w.stride = stride;
-            w.n = count;
-            w.bounces = c->counters;
-            if (it >= 2) HIP_TRY(c, hipStreamWaitEvent(c->stream, c->ev_fold[b], 0));
-            if (it == 0) HIP_TRY(c, hipMemsetAsync(c->queue, 0, 8 * 64, c->stream));  // later: reset by scatter
-            if (lds)
-                hipLaunchKernelGGL(tpt_bdpt_gen_kernel<true>, dim3(gblocks), dim3(kBlock), shmem, c->stream, c->ds, w, it,
-                                   c->queue);
-            else
-                hipLaunchKernelGGL(tpt_bdpt_gen_kernel<false>, dim3(gblocks), dim3(kBlock), shmem, c->stream, c->ds, w, it,
-                                   c->queue);
-            size_t bytes = c->scan_bytes;
-            HIP_TRY(c, rocprim::inclusive_scan(c->scan_tmp, bytes, w.np, w.incl, (size_t)count,
-                                               rocprim::plus<unsigned long long>(),
-                                               c->stream));
-            bytes = c->scan_bytes;
-            HIP_TRY(c, rocprim::inclusive_scan(c->scan_tmp, bytes, w.np2, w.incl2, (size_t)count,
-                                               rocprim::plus<unsigned long long>(), c->stream));
-            hipLaunchKernelGGL(tpt_bdpt_scatter_kernel, dim3(pblocks), dim3(kBlock), 0, c->stream, w, c->queue);
-            HIP_TRY(c, hipEventRecord(c->ev_gen[b], c->stream));
-            HIP_TRY(c, hipStreamWaitEvent(s2, c->ev_gen[b], 0));
-            if (lds)
-                hipLaunchKernelGGL(tpt_bdpt_conn_kernel<true>, dim3(cblocks), dim3(kBlock), shmem, s2, c->ds, w,
-                                   dsplat);
-            else
-                hipLaunchKernelGGL(tpt_bdpt_conn_kernel<false>, dim3(cblocks), dim3(kBlock), shmem, s2, c->ds,
-                                   w, dsplat);
-            hipLaunchKernelGGL(tpt_bdpt_fold_kernel, dim3(pblocks), dim3(kBlock), 0, s2, w, inv);
-            HIP_TRY(c, hipEventRecord(c->ev_fold[b], s2));
+        for (int64_t c0 = 0; c0 < count; c0 += kWfChunk) {
+            rc = launch_bdpt_chunk(c, spp, dlist ? 0 : begin + c0 * stride, stride, std::min(kWfChunk, count - c0),
+                                   dlist ? dlist + c0 : nullptr, dlist ? drows + 3 * c0 : drows, dsplat);
+            if (rc) return rc;
         }
-        HIP_TRY(c, hipStreamWaitEvent(c->stream, c->ev_fold[(spp - 1) & 1], 0));
-        WfState w = c->wf[0];
-        w.list = dlist;
-        w.begin = begin;
-        w.stride = stride;
-        w.n = count;
-        hipLaunchKernelGGL(tpt_bdpt_out_kernel, dim3(pblocks), dim3(kBlock), 0, c->stream, w, drows, dlist ? 1 : 0);
     }
     HIP_TRY(c, hipGetLastError());
     HIP_TRY(c, hipEventRecord(c->ev1, c->stream));
