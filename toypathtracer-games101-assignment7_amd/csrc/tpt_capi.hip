@@ -74,7 +74,7 @@ TPT_D unsigned char* stage_scene(DScene& s) {
 }
 
 #ifndef TPT_PT_MINWAVES
-#define TPT_PT_MINWAVES 4  // waves per SIMD the PT kernel's register budget must allow (4 measured best)
+#define TPT_PT_MINWAVES 5  // waves per SIMD the PT kernel's register budget must allow (measured: 4 / 5 / 6 = 52.9 / 50.8 / 57.1 ms; 5 spills 112 B/lane and still wins)
 #endif
 
 // PT (Renderer.cpp:38-52 with PathTrace), replay-exact, Q lanes per pixel.
@@ -141,7 +141,9 @@ __global__ __launch_bounds__(kBlock, TPT_PT_MINWAVES) void tpt_pt_kernel(DScene 
             // lane's phase, the material type (parked) and the output row are
             // recomputed where they are used, so nothing spills around the loop.
             for (int j0 = 0; j0 < spp; j0 += kQ) {
-                const int qq = lane_id() & (kQ - 1);  // == q: blocks hold whole pixels
+                unsigned ln = threadIdx.x;  // opaque: the lane's phase and shuffle base are
+                asm volatile("" : "+v"(ln));  // recomputed per round, not hoisted and spilled
+                const int qq = (int)(ln & (kQ - 1));  // == q: blocks hold whole pixels
                 V3 L = v3s(0.0f);
                 if (j0 + qq < spp) {
                     L = mul(pt_sample(s, px, rs), inv);
@@ -150,7 +152,7 @@ __global__ __launch_bounds__(kBlock, TPT_PT_MINWAVES) void tpt_pt_kernel(DScene 
                 if (kQ == 1) {
                     acc = acc + L;
                 } else {
-                    const int base = lane_id() - qq;  // first lane of this pixel
+                    const int base = (int)(ln & 63) - qq;  // first lane of this pixel
                     const int n = spp - j0 < kQ ? spp - j0 : kQ;
                     for (int jj = 0; jj < n; ++jj) {
                         acc.x = acc.x + __shfl(L.x, base + jj);

@@ -943,6 +943,13 @@ struct PixPark {
 // direct lighting from every emitter, then the unconditional `break` (:109).
 // The camera hit is the same for every sample of a pixel (no jitter,
 // SceneRenderingHelper.cpp:16-22): the caller computes it once and parks it in `px`.
+// A copy of `a` the compiler cannot see through: values derived from it (the f64
+// conversions of a dot product) are computed after this point, not hoisted out of
+// the emitter loop and held (spilled) across the queries in between.
+TPT_D V3 opaque(V3 a) {
+    asm volatile("" : "+v"(a.x), "+v"(a.y), "+v"(a.z));
+    return a;
+}
 TPT_D V3 pt_sample(const DScene& s, PixPark px, uint32_t& rs) {
     V3 result = v3s(0.0f);
     {
@@ -974,7 +981,7 @@ TPT_D V3 pt_sample(const DScene& s, PixPark px, uint32_t& rs) {
                 V3 hx, hn;
                 hit_geometry(s, rb, hnc, hx, hn);
                 float ld2 = (float)dot3(hx - hx0, hx - hx0);
-                float c = (float)dot3(hn, -wib);
+                float c = (float)dot3(hn, -opaque(wib));
                 if (c != 0.0f) pbl = (float)((double)o.pdf * ld2 / (double)fabs_(c));
             }
             if (pdf_b + pbl > 0.0f) {
@@ -983,7 +990,8 @@ TPT_D V3 pt_sample(const DScene& s, PixPark px, uint32_t& rs) {
                     hit_geometry(s, rb, hb, hx, hn);
                     const bool sh = shadow_ray(s, hx, px.v(kPxX), TPT_CULL_BACK);
                     if (!sh)
-                        ev = ev + divs(eval_bsdf(px.mat(), px.v(kPxWo), wib, px.shade(), true), 1e-4f + pdf_b + pbl);
+                        ev = ev + divs(eval_bsdf(px.mat(), px.v(kPxWo), opaque(wib), px.shade(), true),
+                                       1e-4f + pdf_b + pbl);
                 }
             }
         }
