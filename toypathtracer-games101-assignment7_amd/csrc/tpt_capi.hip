@@ -602,14 +602,25 @@ int launch_bdpt_chunk(tpt_ctx* c, int spp, int64_t begin, int64_t stride, int64_
     HIP_TRY(c, hipEventRecord(c->ev_fold[0], c->stream));
     HIP_TRY(c, hipStreamWaitEvent(s2, c->ev_fold[0], 0));  // stream2 starts after ev0
     const unsigned pblocks = (unsigned)((count + kBlock - 1) / kBlock);
-    const unsigned cblocks = (unsigned)std::min<int64_t>(8192, (count * 24 + kBlock - 1) / kBlock + 1);
+#ifndef TPT_CONN_GRID
+#define TPT_CONN_GRID 8192
+#endif
+    const unsigned cblocks = (unsigned)std::min<int64_t>(TPT_CONN_GRID, (count * 24 + kBlock - 1) / kBlock + 1);
     // persistent gen grid: as many workgroups as are resident at once, a multiple of
     // the 8 queue shards, and no more than the pixels need
     int per_cu = 0;
     HIP_TRY(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(
                    &per_cu, lds ? (const void*)tpt_bdpt_gen_kernel<true> : (const void*)tpt_bdpt_gen_kernel<false>,
                    kBlock, shmem));
-    int64_t gb = (int64_t)std::max(per_cu, 1) * std::max(c->num_cu, 1);
+#ifndef TPT_GEN_GRID_Q
+// gen's persistent grid, in 32nds of what fits on the chip at once.  A full grid
+// occupies every CU until the queue drains, so connect (other stream) only runs in
+// gen's tail; a third of the chip leaves room for both.  Same-box sweep, Standard
+// BDPT 256 spp / bunny BDPT 256 spp: 32 -> 601 ms / -, 8 -> 592 / 1275, 9 -> 564 /
+// 1173, 10 -> 553 / 1131, 11 -> 556 / 1108, 12 -> 567 / -, 16 -> 585 / -.
+#define TPT_GEN_GRID_Q 11
+#endif
+    int64_t gb = (int64_t)std::max(per_cu, 1) * std::max(c->num_cu, 1) * TPT_GEN_GRID_Q / 32;
     gb = std::min<int64_t>(gb, ((int64_t)pblocks + 7) / 8 * 8);
     const unsigned gblocks = (unsigned)std::max<int64_t>(8, gb / 8 * 8);
     const float inv = 1.0f / spp;
