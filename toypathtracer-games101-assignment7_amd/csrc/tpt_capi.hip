@@ -370,15 +370,15 @@ __global__ __launch_bounds__(kBlock) void tpt_bdpt_scatter_kernel(WfState w, uns
     if (k < 8) queue[k * 16] = 0;  // gen of the next iteration (same stream, after this kernel) starts its shards at 0
     if (k >= w.n) return;
     const StratRange r = strat_range(w, k);
-    const int ln = r.ln;
-    for (int pi = 1; pi <= r.np; ++pi) {  // strategy index in (t, s) order; pi = 0 skipped
-        const int t = pi / (ln + 1) + 1, sl = pi % (ln + 1);
-        int64_t g;
-        if (sl == 0) g = r.b[0] + (t - 2);
-        else if (t == 1) g = r.b[3] + (sl - 1);
-        else if (sl == 1) g = r.b[2] + (t - 2);
-        else g = r.b[1] + (int64_t)(t - 2) * (ln - 1) + (sl - 2);
-        w.task[g] = (unsigned)k | (unsigned)t << 22 | (unsigned)sl << 27;
+    const int ln = r.ln, cn = w.cnt[k] & 0xffff;
+    const unsigned kk = (unsigned)k;
+    for (int sl = 1; sl <= ln; ++sl) w.task[r.b[3] + (sl - 1)] = kk | 1u << 22 | (unsigned)sl << 27;  // t = 1
+    for (int t = 2; t <= cn; ++t) {
+        const unsigned kt = kk | (unsigned)t << 22;
+        w.task[r.b[0] + (t - 2)] = kt;                 // s = 0
+        w.task[r.b[2] + (t - 2)] = kt | 1u << 27;      // s = 1
+        const int64_t g1 = r.b[1] + (int64_t)(t - 2) * (ln - 1) - 2;
+        for (int sl = 2; sl <= ln; ++sl) w.task[g1 + sl] = kt | (unsigned)sl << 27;
     }
 }
 
