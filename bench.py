@@ -73,6 +73,8 @@ def parse():
     ap.add_argument("--spp", type=int, default=None, help="override the workload's spp")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline legs")
     ap.add_argument("--no-c5", action="store_true", help="default line without the c5 sub-object")
+    ap.add_argument("--sample-seed", action="store_true",
+                    help="--mode pt|pti only: per-sample seeding (TPT_FLAG_SAMPLE_SEED), a non-replay throughput mode")
     ap.add_argument("--cpu-threads", type=int, default=None)
     return ap.parse_args()
 
@@ -251,13 +253,14 @@ class Runner:
         m = {"pt": pytpt.MODE_PT, "bdpt": pytpt.MODE_BDPT, "pti": pytpt.MODE_PT_INDIRECT}[mode]
         begin, stride = self.sharding.shard(self.rank, self.world)  # Renderer.cpp:38 interleave
         stream = torch.cuda.current_stream()
+        flags = pytpt.FLAG_SAMPLE_SEED if (self.args.sample_seed and self.args.mode in ("pt", "pti")) else 0
 
         def step():
             # libtpt renders on its own stream: everything torch's stream has queued on
             # fb (the zero fill, the previous step's reduce) must finish before it
             # rewrites the buffers.
             stream.synchronize()
-            st = self.ctx.render_device(spp, m, fb[0].data_ptr(), fb[1].data_ptr(), begin, stride)
+            st = self.ctx.render_device(spp, m, fb[0].data_ptr(), fb[1].data_ptr(), begin, stride, flags)
             self.sharding.reduce_frame(self.dist, fb, dst=0)  # rgb + splat onto rank 0 (RCCL over xGMI)
             return st
 
@@ -279,7 +282,8 @@ class Runner:
         kernel_ms = sum(kms) / len(kms)
         shard_samples = st.samples
         tkey = "%s/%s" % (scene, mode)
-        line = {"metric": "Msamples/s (pixels x spp / s), %s %s %dx%d" % (scene, mode.upper(), W, H),
+        line = {"metric": "Msamples/s (pixels x spp / s), %s %s %dx%d%s" % (
+                    scene, mode.upper(), W, H, ", per-sample seeding (not the reference's replay)" if flags else ""),
                 "value": round(samples / dt / 1e6, 2), "unit": "Msamples/s", "n_gpus": self.world, "steps": steps,
                 "warmup": warmup, "ms_per_step": round(dt / steps * 1e3, 3),
                 "config": {"workload": CONFIG_NAME[key] if self.args.mode is None or

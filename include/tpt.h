@@ -68,6 +68,19 @@ extern "C" {
  * reference entry point selects it, and it changes results against HEAD. */
 #define TPT_MODE_PT_INDIRECT 2
 
+/* tpt_render_params.flags.
+ * TPT_FLAG_SAMPLE_SEED: per-sample seeding, a throughput mode that does NOT reproduce
+ * the reference ("per-sample seeding for spp-parallel
+ * throughput"; off by default).  The reference runs one XorShift32 stream per pixel
+ * through all its samples (ResetRandom(i + 1), Renderer.cpp:42); with this flag
+ * sample j of pixel i starts its own stream at tpt_sample_seed(i, j) instead, so the
+ * samples are independent: the estimator is the reference's, the random numbers are
+ * not.  A pixel's samples are then spread over lanes with no stream replay: PT drops
+ * the skip-ahead, PT-indirect runs TPT_PT_LANES lanes per pixel.  The pixel still sums
+ * (1/spp) * L in sample order for PT; PT-indirect sums per lane, then over lanes.
+ * PT and PT-indirect only (BDPT returns TPT_E_UNSUPPORTED). */
+#define TPT_FLAG_SAMPLE_SEED 1
+
 /* Material (Material.hpp:15-44).  `rough` is the already-converted roughness
  * (Material::SetSmoothness -> SmoothnessToRoughenss, GGX.hpp:38-40). */
 typedef struct tpt_material {
@@ -111,7 +124,7 @@ typedef struct tpt_render_params {
     int32_t mode;                 /* TPT_MODE_PT | TPT_MODE_BDPT | TPT_MODE_PT_INDIRECT */
     int64_t pixel_begin;          /* first pixel of this shard (Renderer.cpp:38 `i = off`) */
     int64_t pixel_stride;         /* shard stride (Renderer.cpp:38 `i += j`); 1 = all pixels */
-    int32_t flags;                /* reserved, 0 */
+    int32_t flags;                /* 0, or TPT_FLAG_SAMPLE_SEED */
     int32_t reserved;
 } tpt_render_params;
 
@@ -163,6 +176,10 @@ int tpt_intersect(tpt_ctx* ctx, const float* rays, int64_t n, int32_t cull, floa
 
 /* Camera scale (SceneRenderingHelper.cpp:12-14), computed on the host. */
 float tpt_camera_scale(double fov);
+
+/* The XorShift32 seed of sample j of pixel i under TPT_FLAG_SAMPLE_SEED: the
+ * SplitMix64 finalizer of ((i + 1) << 32 | j), folded to 32 bits (never 0). */
+uint32_t tpt_sample_seed(int64_t pixel, int32_t sample);
 
 /* ---- multi-GPU (one process, the GPUs of one node) ---------------------------
  * Replaces Renderer::Render's worker split and splat merge (Renderer.cpp:86-114)

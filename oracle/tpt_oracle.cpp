@@ -1230,6 +1230,41 @@ static void trace_pixel(const Scene& sc, float scale, int mode, int spp, int64_t
     if (bounces) *bounces = nb;
 }
 
+// TPT_FLAG_SAMPLE_SEED (include/tpt.h): not the reference's seeding -- sample j of
+// pixel i starts its own XorShift32 stream (SplitMix64 finalizer of ((i+1) << 32 | j),
+// folded to 32 bits, never 0); everything else is the reference's per-sample
+// estimator.  `lanes` = how the library spreads a pixel's samples: 1 sums (1/spp) * L
+// in sample order (PT), L > 1 sums per lane q over samples j = q, q + L, ... and then
+// the L partial sums in lane order (PT-indirect with TPT_PT_LANES lanes).
+static uint32_t sample_seed(int64_t i, int j) {
+    uint64_t z = ((uint64_t)(i + 1) << 32 | (uint32_t)j) + 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    const uint32_t r = (uint32_t)z ^ (uint32_t)(z >> 32);
+    return r ? r : 0x6B43A9B5u;
+}
+static void trace_pixel_seeded(const Scene& sc, float scale, int mode, int spp, int64_t i, int lanes, float* out,
+                               int64_t* bounces) {
+    int px = (int)(i % sc.width), py = (int)(i / sc.width);
+    V3 acc(0.0f);
+    int64_t nb = 0;
+    for (int q = 0; q < lanes; ++q) {
+        V3 part(0.0f);
+        for (int s = q; s < spp; s += lanes) {
+            rnd_state = sample_seed(i, s);
+            V3 dir = pixel_ray(px, py, sc.width, sc.height, scale);
+            int b = 0;
+            V3 L = mode == TPT_MODE_PT_INDIRECT ? path_trace_indirect(sc, Ray(sc.eye, dir), b) : path_trace(sc, Ray(sc.eye, dir), b);
+            part = part + mul(L, 1.0f / spp);
+            nb += b;
+        }
+        acc = lanes == 1 ? part : acc + part;
+    }
+    out[0] = acc.x; out[1] = acc.y; out[2] = acc.z;
+    if (bounces) *bounces = nb;
+}
+
 }  // namespace orc
 
 using namespace orc;
@@ -1266,6 +1301,16 @@ void oracle_trace_pixels(void* h, int mode, int spp, const int64_t* pix, int64_t
             splat[3 * i] = e.x; splat[3 * i + 1] = e.y; splat[3 * i + 2] = e.z;
         }
 }
+
+// TPT_FLAG_SAMPLE_SEED restated (see trace_pixel_seeded); PT / PT-indirect only.
+void oracle_trace_pixels_seeded(void* h, int mode, int spp, const int64_t* pix, int64_t n, int lanes, float* out,
+                                int64_t* bounces) {
+    Scene* s = (Scene*)h;
+    float scale = camera_scale(s->fov);
+    for (int64_t k = 0; k < n; ++k)
+        trace_pixel_seeded(*s, scale, mode, spp, pix[k], lanes, out + 3 * k, bounces ? bounces + k : nullptr);
+}
+uint32_t oracle_sample_seed(int64_t i, int j) { return sample_seed(i, j); }
 
 // Renderer::Render (Renderer.cpp:68-127): `threads` workers on the interleaved
 // pixel split, per-thread splat buffers merged in thread order.  Used as the

@@ -33,6 +33,9 @@ class Oracle:
         L.oracle_create.argtypes = [P]
         L.oracle_destroy.argtypes = [P]
         L.oracle_trace_pixels.argtypes = [P, ctypes.c_int, ctypes.c_int, P, ctypes.c_int64, P, P, P]
+        L.oracle_trace_pixels_seeded.argtypes = [P, ctypes.c_int, ctypes.c_int, P, ctypes.c_int64, ctypes.c_int, P, P]
+        L.oracle_sample_seed.argtypes = [ctypes.c_int64, ctypes.c_int32]
+        L.oracle_sample_seed.restype = ctypes.c_uint32
         L.oracle_render.argtypes = [P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int64, P]
         L.oracle_render.restype = ctypes.c_double
         L.oracle_rng.argtypes = [ctypes.c_uint32, ctypes.c_int, P, P]
@@ -59,6 +62,18 @@ class Oracle:
         b = np.zeros(len(pix), np.int64)
         self.L.oracle_trace_pixels(P(self.h), mode, spp, _p(pix), len(pix), _p(out), _p(splat), _p(b))
         return out, (splat.reshape(self.height, self.width, 3) if want_splat else None), b
+
+    def trace_pixels_seeded(self, mode, spp, pix, lanes=1):
+        """TPT_FLAG_SAMPLE_SEED restated (oracle_trace_pixels_seeded): PT with lanes=1,
+        PT-indirect with the library's TPT_PT_LANES."""
+        pix = np.ascontiguousarray(pix, np.int64)
+        out = np.zeros((len(pix), 3), np.float32)
+        b = np.zeros(len(pix), np.int64)
+        self.L.oracle_trace_pixels_seeded(P(self.h), mode, spp, _p(pix), len(pix), lanes, _p(out), _p(b))
+        return out, b
+
+    def sample_seed(self, i, j):
+        return int(self.L.oracle_sample_seed(ctypes.c_int64(i), ctypes.c_int32(j)))
 
     def traversal_counts(self, mode, spp, pix):
         """(nodes popped, triangle tests) summed over `pix` x `spp` (SURVEY §8(d) B_alg)."""

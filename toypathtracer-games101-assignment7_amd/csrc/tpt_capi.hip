@@ -111,7 +111,9 @@ TPT_D uint32_t skip_samples(uint32_t st, int type, int light_draws, int n) {
 constexpr int kQ = TPT_PT_LANES;
 static_assert(kQ == 1 || kQ == 2 || kQ == 4 || kQ == 8 || kQ == 16, "Q must be a power of two dividing the wave");
 
-template <bool kLds>
+// kSeeded: TPT_FLAG_SAMPLE_SEED -- each sample seeds its own stream (sample_seed), so
+// no lane steps past the other lanes' samples.
+template <bool kLds, bool kSeeded>
 __global__ __launch_bounds__(kBlock, TPT_PT_MINWAVES) void tpt_pt_kernel(DScene s, int spp, int64_t begin,
                                                                         int64_t stride, int64_t count,
                                                                         const int64_t* __restrict__ list,
@@ -136,7 +138,7 @@ __global__ __launch_bounds__(kBlock, TPT_PT_MINWAVES) void tpt_pt_kernel(DScene 
             px.park(v.x, v.N, -dir, mi, m);
             const float inv = 1.0f / spp;
             uint32_t rs = (uint32_t)((int)i + 1);  // ResetRandom(i + 1), Renderer.cpp:42
-            rs = skip_samples(rs, m.type, s.light_draws, q);
+            if (!kSeeded) rs = skip_samples(rs, m.type, s.light_draws, q);
             // Only acc, rs and the loop counter stay live across the sample loop: the
             // lane's phase, the material type (parked) and the output row are
             // recomputed where they are used, so nothing spills around the loop.
@@ -146,8 +148,12 @@ __global__ __launch_bounds__(kBlock, TPT_PT_MINWAVES) void tpt_pt_kernel(DScene 
                 const int qq = (int)(ln & (kQ - 1));  // == q: blocks hold whole pixels
                 V3 L = v3s(0.0f);
                 if (j0 + qq < spp) {
+                    if (kSeeded) {
+                        const int64_t kk = ((int64_t)blockIdx.x * kBlock + ln) / kQ;
+                        rs = sample_seed(list ? list[kk] : begin + kk * stride, j0 + qq);
+                    }
                     L = mul(pt_sample(s, px, rs), inv);
-                    if (kQ > 1) rs = skip_samples(rs, px.type(), s.light_draws, kQ - 1);
+                    if (kQ > 1 && !kSeeded) rs = skip_samples(rs, px.type(), s.light_draws, kQ - 1);
                 }
                 if (kQ == 1) {
                     acc = acc + L;
@@ -191,20 +197,27 @@ constexpr int kPtiMaxBounces = 1 << 16;
 // the next sample starts in the same iteration, so lanes of a wave never wait for
 // one another's long paths until the pixel's last sample (per-lane regeneration,
 // in registers).
-template <bool kLds>
+//
+// kSeeded (TPT_FLAG_SAMPLE_SEED): samples are independent, so kQ lanes share a pixel:
+// lane q runs samples q, q + kQ, ... back to back (each from sample_seed), sums its
+// own (1/spp) * L, and the kQ partial sums are added in lane order at the end.
+template <bool kLds, bool kSeeded>
 __global__ __launch_bounds__(kBlock, TPT_PTI_MINWAVES) void tpt_pti_kernel(DScene s, int spp, int64_t begin,
                                                                           int64_t stride, int64_t count,
                                                                           const int64_t* __restrict__ list,
                                                                           float* __restrict__ out,
                                                                           unsigned long long* __restrict__ bounces) {
     stage_scene<kLds>(s);
-    const int64_t k = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    constexpr int kL = kSeeded ? kQ : 1;  // lanes per pixel
+    const int64_t gl = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const int64_t k = gl / kL;
+    const int q = (int)(gl % kL);
     const bool on = k < count;
     const int64_t i = on ? (list ? list[k] : begin + k * stride) : 0;
     const V3 eye = v3(s.eye[0], s.eye[1], s.eye[2]);
     const V3 dir = pixel_ray((int)(i % s.width), (int)(i / s.width), s.width, s.height, s.scale);
     const float inv = 1.0f / spp;
-    uint32_t rs = (uint32_t)((int)i + 1);  // ResetRandom(i + 1), Renderer.cpp:42
+    uint32_t rs = kSeeded ? sample_seed(i, q) : (uint32_t)((int)i + 1);  // ResetRandom(i + 1), Renderer.cpp:42
     V3 acc = v3s(0.0f);
     PtiPath p;
     p.r = make_ray(eye, dir);
@@ -213,7 +226,7 @@ __global__ __launch_bounds__(kBlock, TPT_PTI_MINWAVES) void tpt_pti_kernel(DScen
     p.nb = 0;
     p.flip = false;
     unsigned long long nbt = 0;
-    for (int j = on ? 0 : spp; j < spp;) {
+    for (int j = on ? q : spp; j < spp;) {
         bool live = !(p.alpha.x == 0.0f && p.alpha.y == 0.0f && p.alpha.z == 0.0f) && p.nb < kPtiMaxBounces;  // :54-55
         if (live) {
             const PTV v = scene_intersect(s, p.r, p.flip ? TPT_CULL_FRONT : TPT_CULL_BACK);  // :56
@@ -222,7 +235,8 @@ __global__ __launch_bounds__(kBlock, TPT_PTI_MINWAVES) void tpt_pti_kernel(DScen
         if (!live) {
             acc = acc + mul(p.res, inv);  // Renderer.cpp:49 `fb[i] += (1.0f / spp) * L`
             nbt += (unsigned long long)p.nb;
-            ++j;
+            j += kL;
+            if (kSeeded && j < spp) rs = sample_seed(i, j);
             p.r = make_ray(eye, dir);
             p.alpha = v3s(1.0f);
             p.res = v3s(0.0f);
@@ -230,7 +244,17 @@ __global__ __launch_bounds__(kBlock, TPT_PTI_MINWAVES) void tpt_pti_kernel(DScen
             p.flip = false;
         }
     }
-    if (on) {
+    if (kSeeded) {  // the pixel's kL partial sums, in lane order (blocks hold whole pixels)
+        const int base = lane_id() - q;
+        V3 t = v3s(0.0f);
+        for (int jj = 0; jj < kL; ++jj) {
+            t.x = t.x + __shfl(acc.x, base + jj);
+            t.y = t.y + __shfl(acc.y, base + jj);
+            t.z = t.z + __shfl(acc.z, base + jj);
+        }
+        acc = t;
+    }
+    if (on && q == 0) {
         const int64_t row = list ? k : i;
         out[3 * row + 0] = acc.x;
         out[3 * row + 1] = acc.y;
@@ -670,8 +694,9 @@ int launch_bdpt_chunk(tpt_ctx* c, int spp, int64_t begin, int64_t stride, int64_
 }
 
 // Launch the integration kernel for `count` pixels; rows/splat are device buffers.
-int launch(tpt_ctx* c, int mode, int spp, int64_t begin, int64_t stride, int64_t count, const int64_t* dlist,
-           float* drows, float* dsplat, tpt_stats* st) {
+int launch(tpt_ctx* c, int mode, int flags, int spp, int64_t begin, int64_t stride, int64_t count,
+           const int64_t* dlist, float* drows, float* dsplat, tpt_stats* st) {
+    const bool seeded = (flags & TPT_FLAG_SAMPLE_SEED) != 0;
     if (st) std::memset(st, 0, sizeof(*st));  // an empty shard or list reports zeros
     if (count <= 0) {  // nothing to trace; the caller's memsets still complete before returning
         HIP_TRY(c, hipStreamSynchronize(c->stream));
@@ -685,19 +710,16 @@ int launch(tpt_ctx* c, int mode, int spp, int64_t begin, int64_t stride, int64_t
     if (mode == TPT_MODE_PT) {
         const int64_t qblocks = (count * kQ + kBlock - 1) / kBlock;
         const size_t pshmem = shmem + (size_t)kPixSlots * kBlock * sizeof(float);
-        if (lds)
-            hipLaunchKernelGGL(tpt_pt_kernel<true>, dim3((unsigned)qblocks), dim3(kBlock), pshmem, c->stream, c->ds,
-                               spp, begin, stride, count, dlist, drows);
-        else
-            hipLaunchKernelGGL(tpt_pt_kernel<false>, dim3((unsigned)qblocks), dim3(kBlock), pshmem, c->stream, c->ds,
-                               spp, begin, stride, count, dlist, drows);
+        auto k = lds ? (seeded ? tpt_pt_kernel<true, true> : tpt_pt_kernel<true, false>)
+                     : (seeded ? tpt_pt_kernel<false, true> : tpt_pt_kernel<false, false>);
+        hipLaunchKernelGGL(k, dim3((unsigned)qblocks), dim3(kBlock), pshmem, c->stream, c->ds, spp, begin, stride,
+                           count, dlist, drows);
     } else if (mode == TPT_MODE_PT_INDIRECT) {
-        if (lds)
-            hipLaunchKernelGGL(tpt_pti_kernel<true>, dim3((unsigned)blocks), dim3(kBlock), shmem, c->stream, c->ds, spp,
-                               begin, stride, count, dlist, drows, c->counters);
-        else
-            hipLaunchKernelGGL(tpt_pti_kernel<false>, dim3((unsigned)blocks), dim3(kBlock), shmem, c->stream, c->ds,
-                               spp, begin, stride, count, dlist, drows, c->counters);
+        const int64_t lanes = count * (seeded ? kQ : 1);
+        auto k = lds ? (seeded ? tpt_pti_kernel<true, true> : tpt_pti_kernel<true, false>)
+                     : (seeded ? tpt_pti_kernel<false, true> : tpt_pti_kernel<false, false>);
+        hipLaunchKernelGGL(k, dim3((unsigned)((lanes + kBlock - 1) / kBlock)), dim3(kBlock), shmem, c->stream, c->ds,
+                           spp, begin, stride, count, dlist, drows, c->counters);
     } else {
         // Shards larger than kWfChunk pixel streams run as consecutive wavefronts.
         int rc = ensure_wf(c, std::min(count, kWfChunk));
@@ -730,12 +752,15 @@ int launch(tpt_ctx* c, int mode, int spp, int64_t begin, int64_t stride, int64_t
     return TPT_OK;
 }
 
-int check_render_args(tpt_ctx* c, int spp, int mode) {
+int check_render_args(tpt_ctx* c, int spp, int mode, int flags = 0) {
     if (!c) return TPT_E_INVALID;
     if (!c->has_scene) return fail(c, TPT_E_NOSCENE, "no scene uploaded");
     if (spp <= 0) return fail(c, TPT_E_INVALID, "spp must be positive");
     if (mode != TPT_MODE_PT && mode != TPT_MODE_BDPT && mode != TPT_MODE_PT_INDIRECT)
         return fail(c, TPT_E_INVALID, "unknown mode");
+    if (flags & ~TPT_FLAG_SAMPLE_SEED) return fail(c, TPT_E_INVALID, "unknown flags");
+    if ((flags & TPT_FLAG_SAMPLE_SEED) && mode == TPT_MODE_BDPT)
+        return fail(c, TPT_E_UNSUPPORTED, "per-sample seeding (TPT_FLAG_SAMPLE_SEED) is for PT and PT-indirect");
     if (mode == TPT_MODE_BDPT && c->hs.emitters.empty())
         return fail(c, TPT_E_INVALID, "BDPT needs an emitter (BDPT.cpp:287 uses m_emissionObjects[0])");
     return TPT_OK;
@@ -747,6 +772,7 @@ extern "C" {
 
 int tpt_abi_version(void) { return TPT_ABI_VERSION; }
 float tpt_camera_scale(double fov) { return camera_scale(fov); }
+uint32_t tpt_sample_seed(int64_t pixel, int32_t sample) { return sample_seed(pixel, sample); }
 
 int tpt_create(int device, tpt_ctx** out) {
     if (!out) return TPT_E_INVALID;
@@ -895,7 +921,7 @@ int tpt_upload_scene(tpt_ctx* c, const tpt_scene_desc* d) {
 
 int tpt_render_device(tpt_ctx* c, const tpt_render_params* p, float* rgb_dev, float* splat_dev, tpt_stats* st) {
     if (!c || !p) return TPT_E_INVALID;
-    int rc = check_render_args(c, p->spp, p->mode);
+    int rc = check_render_args(c, p->spp, p->mode, p->flags);
     if (rc) return rc;
     if (p->pixel_begin < 0 || p->pixel_stride < 1) return fail(c, TPT_E_INVALID, "bad pixel shard");
     if (!rgb_dev || (p->mode == TPT_MODE_BDPT && !splat_dev)) return fail(c, TPT_E_INVALID, "null output buffer");
@@ -905,7 +931,7 @@ int tpt_render_device(tpt_ctx* c, const tpt_render_params* p, float* rgb_dev, fl
     HIP_TRY(c, hipMemsetAsync(rgb_dev, 0, npix * 3 * sizeof(float), c->stream));
     if (p->mode == TPT_MODE_BDPT) HIP_TRY(c, hipMemsetAsync(splat_dev, 0, npix * 3 * sizeof(float), c->stream));
     const int64_t count = shard_count(npix, p->pixel_begin, p->pixel_stride);
-    rc = launch(c, p->mode, p->spp, p->pixel_begin, p->pixel_stride, count, nullptr, rgb_dev,
+    rc = launch(c, p->mode, p->flags, p->spp, p->pixel_begin, p->pixel_stride, count, nullptr, rgb_dev,
                 p->mode == TPT_MODE_BDPT ? splat_dev : nullptr, st);
     if (rc) return rc;
     if (st) st->total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
@@ -914,7 +940,7 @@ int tpt_render_device(tpt_ctx* c, const tpt_render_params* p, float* rgb_dev, fl
 
 int tpt_render(tpt_ctx* c, const tpt_render_params* p, float* rgb, float* splat, tpt_stats* st) {
     if (!c || !p || !rgb) return TPT_E_INVALID;
-    int rc = check_render_args(c, p->spp, p->mode);
+    int rc = check_render_args(c, p->spp, p->mode, p->flags);
     if (rc) return rc;
     auto t0 = std::chrono::steady_clock::now();
     rc = tpt_render_device(c, p, c->rgb, c->splat, st);
@@ -946,7 +972,7 @@ int tpt_render_pixels(tpt_ctx* c, int32_t spp, int32_t mode, const int64_t* pixe
     }
     if (n > 0) HIP_TRY(c, hipMemcpyAsync(c->list, pixels, n * sizeof(int64_t), hipMemcpyHostToDevice, c->stream));
     if (mode == TPT_MODE_BDPT) HIP_TRY(c, hipMemsetAsync(c->splat, 0, npix * 3 * sizeof(float), c->stream));
-    rc = launch(c, mode, spp, 0, 1, n, c->list, c->rows, mode == TPT_MODE_BDPT ? c->splat : nullptr, st);
+    rc = launch(c, mode, 0, spp, 0, 1, n, c->list, c->rows, mode == TPT_MODE_BDPT ? c->splat : nullptr, st);
     if (rc) return rc;
     if (n > 0) HIP_TRY(c, hipMemcpy(rgb, c->rows, n * 3 * sizeof(float), hipMemcpyDeviceToHost));
     if (mode == TPT_MODE_BDPT && splat)

@@ -140,6 +140,17 @@ TPT_HD uint32_t xorshift32(uint32_t& s) {
 TPT_HD float rng_float(uint32_t& s) {
     return (float)((double)xorshift32(s) * (1.0 / 4294967295.0));
 }
+// TPT_FLAG_SAMPLE_SEED (include/tpt.h): sample j of pixel i starts its own stream.
+// SplitMix64's finalizer of ((i + 1) << 32 | j), folded to 32 bits, never 0
+// (a zero XorShift32 state stays zero).  Not the reference's seeding.
+TPT_HD uint32_t sample_seed(int64_t i, int j) {
+    uint64_t z = ((uint64_t)(i + 1) << 32 | (uint32_t)j) + 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    const uint32_t s = (uint32_t)z ^ (uint32_t)(z >> 32);
+    return s ? s : 0x6B43A9B5u;
+}
 
 // --------------------------------------------------- glibc float libm -----
 // sinf / cosf: glibc 2.35 flt-32 s_sinf.c / s_cosf.c; polynomial table

@@ -22,6 +22,7 @@ TPT_E_ALLOC = -4
 TPT_E_UNSUPPORTED = -5
 MODE_PT, MODE_BDPT = 0, 1
 MODE_PT_INDIRECT = 2  # PathTrace without the HEAD `break` (PathTracer.cpp:109); off by default
+FLAG_SAMPLE_SEED = 1  # per-sample seeding (tpt.h TPT_FLAG_SAMPLE_SEED): a non-replay throughput mode
 CULL_BACK, CULL_FRONT, NO_CULL = 0, 1, 2
 PRESETS = ("silver", "standard", "refractive_ball", "occlusion", "smooth_dielectric", "bunny")
 EDGE_PRESETS = ("multi_light", "emissive_sphere", "background")
@@ -58,7 +59,7 @@ class Stats(ctypes.Structure):
 
 # Every symbol declared in include/tpt.h and include/tpt_host.h.
 EXPORTS = ("tpt_create", "tpt_destroy", "tpt_last_error", "tpt_abi_version", "tpt_upload_scene", "tpt_render",
-           "tpt_render_pixels", "tpt_render_device", "tpt_intersect", "tpt_camera_scale",
+           "tpt_render_pixels", "tpt_render_device", "tpt_intersect", "tpt_camera_scale", "tpt_sample_seed",
            "tpt_multi_create", "tpt_multi_destroy", "tpt_multi_last_error", "tpt_multi_upload_scene",
            "tpt_render_multi",
            "tpt_preset_load", "tpt_preset_desc", "tpt_preset_free", "tpt_save_image")
@@ -88,6 +89,8 @@ def lib():
     L.tpt_intersect.argtypes = [P, P, ctypes.c_int64, ctypes.c_int32, P]
     L.tpt_camera_scale.argtypes = [ctypes.c_double]
     L.tpt_camera_scale.restype = ctypes.c_float
+    L.tpt_sample_seed.argtypes = [ctypes.c_int64, ctypes.c_int32]
+    L.tpt_sample_seed.restype = ctypes.c_uint32
     L.tpt_preset_load.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int32, ctypes.c_int32,
                                   ctypes.POINTER(P)]
     L.tpt_preset_desc.argtypes = [P]
@@ -157,11 +160,11 @@ class Context:
         self.width, self.height = desc.contents.width, desc.contents.height
         self._keep = preset_or_desc
 
-    def render(self, spp, mode=MODE_PT, begin=0, stride=1):
+    def render(self, spp, mode=MODE_PT, begin=0, stride=1, flags=0):
         n = self.width * self.height * 3
         rgb = np.zeros(n, np.float32)
         splat = np.zeros(n, np.float32) if mode == MODE_BDPT else None
-        p = RenderParams(spp, mode, begin, stride, 0, 0)
+        p = RenderParams(spp, mode, begin, stride, flags, 0)
         st = Stats()
         self._check(lib().tpt_render(self.h, ctypes.byref(p), _ptr(rgb), _ptr(splat), ctypes.byref(st)),
                     "tpt_render")
@@ -170,8 +173,8 @@ class Context:
             splat = splat.reshape(self.height, self.width, 3)
         return rgb, splat, st
 
-    def render_device(self, spp, mode, rgb_dev_ptr, splat_dev_ptr, begin=0, stride=1):
-        p = RenderParams(spp, mode, begin, stride, 0, 0)
+    def render_device(self, spp, mode, rgb_dev_ptr, splat_dev_ptr, begin=0, stride=1, flags=0):
+        p = RenderParams(spp, mode, begin, stride, flags, 0)
         st = Stats()
         self._check(lib().tpt_render_device(self.h, ctypes.byref(p), ctypes.c_void_p(rgb_dev_ptr),
                                             ctypes.c_void_p(splat_dev_ptr) if splat_dev_ptr else None,
