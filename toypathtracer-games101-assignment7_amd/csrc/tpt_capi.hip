@@ -702,7 +702,6 @@ int launch(tpt_ctx* c, int mode, int flags, int spp, int64_t begin, int64_t stri
         HIP_TRY(c, hipStreamSynchronize(c->stream));
         return TPT_OK;
     }
-    const int64_t blocks = (count + kBlock - 1) / kBlock;
     HIP_TRY(c, hipMemsetAsync(c->counters, 0, sizeof(unsigned long long) * 32, c->stream));
     HIP_TRY(c, hipEventRecord(c->ev0, c->stream));
     const bool lds = c->ds.lds_bytes > 0;
