@@ -119,6 +119,7 @@ __global__ __launch_bounds__(kBlock, TPT_PT_MINWAVES) void tpt_pt_kernel(DScene 
                                                                         const int64_t* __restrict__ list,
                                                                         float* __restrict__ out) {
     unsigned char* lds_free = stage_scene<kLds>(s);
+    s.qs = nullptr;  // coherent rays: the per-leaf flat loops (the compacted form's code folds away)
     V3 acc = v3s(0.0f);
     {
         const int64_t gl = (int64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -208,6 +209,7 @@ __global__ __launch_bounds__(kBlock, TPT_PTI_MINWAVES) void tpt_pti_kernel(DScen
                                                                           float* __restrict__ out,
                                                                           unsigned long long* __restrict__ bounces) {
     stage_scene<kLds>(s);
+    s.qs = nullptr;
     constexpr int kL = kSeeded ? kQ : 1;  // lanes per pixel
     const int64_t gl = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     const int64_t k = gl / kL;
@@ -283,6 +285,8 @@ template <bool kLds>
 __global__ __launch_bounds__(kBlock, TPT_GEN_MINWAVES) void tpt_bdpt_gen_kernel(DScene s, WfState w, int iter,
                                                                                unsigned* __restrict__ queue) {
     stage_scene<kLds>(s);
+    __shared__ QScratch qsm[kBlock / 64];  // compacted flat queries (tpt_device.h)
+    s.qs = qsm;
     const int shard = blockIdx.x & 7;
     const int64_t k_lo = w.n * shard / 8, k_hi = w.n * (shard + 1) / 8;
     unsigned* q = queue + shard * 16;  // 64 B apart
@@ -411,6 +415,8 @@ __global__ __launch_bounds__(kBlock) void tpt_bdpt_scatter_kernel(WfState w, uns
 template <bool kLds>
 __global__ __launch_bounds__(kBlock, TPT_CONN_MINWAVES) void tpt_bdpt_conn_kernel(DScene s, WfState w, float* __restrict__ splat) {
     stage_scene<kLds>(s);
+    __shared__ QScratch qsm[kBlock / 64];
+    s.qs = qsm;
     const int64_t total = total_tasks(w);
     const V3 eye = v3(s.eye[0], s.eye[1], s.eye[2]);
     for (int64_t g0 = (int64_t)blockIdx.x * kBlock + (threadIdx.x & ~63); g0 < total;
@@ -482,6 +488,8 @@ __global__ void tpt_scale_kernel(float* __restrict__ buf, int64_t n, float spp) 
 // Closest-hit queries (Scene::Intersect) for tpt_intersect.
 __global__ __launch_bounds__(kBlock) void tpt_intersect_kernel(DScene s, const float* __restrict__ rays, int64_t n,
                                                                int cull, float* __restrict__ out) {
+    __shared__ QScratch qsm[kBlock / 64];
+    s.qs = qsm;
     const int64_t k = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (k >= n) return;
     const float* q = rays + 6 * k;

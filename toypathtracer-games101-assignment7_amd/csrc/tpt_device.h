@@ -205,7 +205,7 @@ TPT_D Hit traverse_t(const DScene& s, int root, const Ray& r, int cull) {
 // when some lane's box passed.  For scenes with few leaves (the Cornell presets: 32
 // triangles) this beats a per-lane walk; rays with an infinite inv component keep
 // the walk.
-enum { kFlatShadow = 1, kFlatHit = 2 };  // DScene::flat bits
+enum { kFlatShadow = 1, kFlatHit = 2, kFlatCompactAll = 4 };  // DScene::flat bits (4: tests force the compacted form)
 // A walk group (groups[g].b < 0) is a mesh too large for the flat list (the bunny):
 // a lane whose ray passed the group box -- the mesh root's box, tpt_scene.h -- walks
 // the mesh's threaded subtree from the root's right child (a) until kMeshExit, i.e.
@@ -313,9 +313,248 @@ TPT_D bool shadow_flat(const DScene& s, const Ray& r, V3 lc, double thr, int cul
     return sh;
 }
 
+// ---- compacted flat queries (the BDPT kernels) --------------------------------
+// In the loops above a primitive test runs for the whole wave as soon as ONE lane's
+// ray passes the leaf box.  Waves of incoherent rays (BDPT's path extensions and
+// connections) pass almost every leaf box somewhere in the wave while each ray passes
+// only a few: Standard, uniform surface-to-surface rays pass 4.4 of 32 leaf boxes
+// per ray but 31.4 per wave of 64, so most lanes of most primitive tests idle.  The
+// compacted form splits the query:
+//   1. each lane slab-tests the leaves (wave-uniform loop, as above) into a 64-bit
+//      mask of the leaves its ray passes (kFlatMaxLeaves = 64);
+//   2. the (ray, leaf) pairs are listed in LDS, lane-major and in leaf order within a
+//      lane, and dealt densely to the active lanes: a lane takes pair p, fetches the
+//      owner's ray with ds_bpermute and runs the same primitive test on it;
+//   3. the owner folds its pairs' results in leaf order: the sequential strict-`>`
+//      update of BVHAccel::Intersect (BVH.cpp:103-143) for a closest hit, any hit
+//      below the threshold for a shadow query.
+// Same (ray, primitive) pairs, the same tests on bit-identical operands and, per ray,
+// the same order: the result is the flat loop's, bit for bit.  A wave whose rays are
+// coherent (few leaves passed, by many lanes each) keeps the per-leaf loop; the
+// choice is made per wave and query.
+constexpr int kQC = 256;  // pair slots per chunk
+struct QScratch {         // per wave, in LDS
+    uint16_t pair[kQC];   // owner lane | leaf << 6
+    double res[kQC];      // closest hit: the pair's distance, -1 for no hit
+    uint32_t flag[64];    // shadow query: the owner's ray is blocked
+};
+TPT_D QScratch* wave_qs(const DScene& s) { return reinterpret_cast<QScratch*>(s.qs) + (threadIdx.x >> 6); }
+// LDS writes of some lanes made visible to reads of other lanes of the same wave
+TPT_D void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+TPT_D int mbcnt64(uint64_t m) {
+    return (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+}
+// Step 1 over the flat groups [g0, g1): `mask` = leaves this lane's ray passes, `any`
+// (wave-uniform) = leaves some lane's ray passes.  A leaf box passing implies its
+// group box passes (the group box is the union), so `pass &&` changes nothing.
+TPT_D void leaf_masks(const DScene& s, int g0, int g1, const Ray& r, bool on, uint64_t& mask, uint64_t& any) {
+    mask = 0;
+    any = 0;
+    for (int gi = g0; gi < g1; ++gi) {
+        const DNode gn = s.groups[gi];
+        if (gn.b < 0) continue;  // walk group: handled by the caller
+        const bool pass = on && slab_hit_finite(gn.bmin[0], gn.bmin[1], gn.bmin[2], gn.bmax[0], gn.bmax[1], gn.bmax[2], r);
+        if (__ballot(pass) == 0) continue;
+        const int j1 = gn.a + gn.b;
+        for (int j = gn.a; j < j1; ++j) {
+            const DNode n = s.leaves[j];
+            const bool p = pass && slab_hit_finite(n.bmin[0], n.bmin[1], n.bmin[2], n.bmax[0], n.bmax[1], n.bmax[2], r);
+            if (__ballot(p) != 0) any |= 1ull << j;
+            if (p) mask |= 1ull << j;
+        }
+    }
+}
+// Step 2's plan: this lane's pairs occupy slots [off, off + cnt) of the wave's list
+// (exclusive prefix over the active lanes, from ballots of the count's bits, so
+// inactive lanes count for nothing); n pairs in all, dealt over the na active lanes.
+struct QPlan {
+    int off, cnt, n, na, rank;
+};
+TPT_D QPlan q_plan(uint64_t mask) {
+    QPlan q;
+    q.cnt = __popcll(mask);
+    q.off = 0;
+    q.n = 0;
+    for (int b = 0; b < 7; ++b) {
+        const uint64_t m = __ballot((q.cnt >> b) & 1);
+        q.off += mbcnt64(m) << b;
+        q.n += __popcll(m) << b;
+    }
+    const uint64_t act = __ballot(true);
+    q.na = __popcll(act);
+    q.rank = mbcnt64(act);
+    return q;
+}
+// Dense rounds beat one wave-wide test per passed leaf by a wide margin or not at all.
+TPT_D bool q_compact_pays(const DScene& s, const QPlan& q, uint64_t any) {
+    const int rounds = (q.n + q.na - 1) / q.na;
+    return (s.flat & kFlatCompactAll) || (rounds + 1) * 5 < __popcll(any) * 4;
+}
+// The primitive test of flat leaf n (as in traverse_flat / shadow_flat).
+TPT_D bool leaf_test(const DScene& s, const DNode& n, const Ray& r, int cull, double& dist) {
+    const int prim = -1 - n.a;
+    if (prim < s.ntri) return tri_test(s.ftris[n.b], r, cull, dist);
+    return sphere_test(s.sph[prim - s.ntri], r, cull, dist);
+}
+TPT_D V3 shfl3(V3 a, int l) { return v3(__shfl(a.x, l), __shfl(a.y, l), __shfl(a.z, l)); }
+// Step 2a for the chunk of slots [c0, c1): each lane writes its pairs that fall in it
+// (mw / sw: its leaves and the slot of the next pair still to be listed).
+TPT_D void q_list(QScratch* qs, int c0, int c1, int end, uint64_t& mw, int& sw) {
+    const int lane = (int)__lane_id();
+    while (sw < end && sw < c1) {
+        const int j = __builtin_ctzll(mw);
+        mw &= mw - 1;
+        qs->pair[sw - c0] = (uint16_t)(lane | j << 6);
+        ++sw;
+    }
+    wave_lds_sync();
+}
+
+// Closest hit over the flat groups [g0, g1), folded into `best` (which already holds
+// the hits of the leaves before g0, in the reference's order).
+TPT_D void flat_closest_c(const DScene& s, int g0, int g1, const Ray& r, int cull, Hit& best) {
+    uint64_t mask, any;
+    leaf_masks(s, g0, g1, r, true, mask, any);
+    if (any == 0) return;
+    const QPlan q = q_plan(mask);
+    if (!q_compact_pays(s, q, any)) {
+        for (uint64_t m = any; m != 0; m &= m - 1) {
+            const int j = __builtin_ctzll(m);
+            if ((mask >> j) & 1) {
+                const DNode n = s.leaves[j];
+                double dist;
+                if (leaf_test(s, n, r, cull, dist) && (best.prim < 0 || best.dist > dist)) {
+                    best.dist = dist;
+                    best.prim = -1 - n.a;
+                }
+            }
+        }
+        return;
+    }
+    QScratch* qs = wave_qs(s);
+    uint64_t mw = mask, mr = mask;
+    int sw = q.off, sr = q.off;
+    const int end = q.off + q.cnt;
+    for (int c0 = 0; c0 < q.n; c0 += kQC) {
+        const int c1 = c0 + kQC < q.n ? c0 + kQC : q.n;
+        q_list(qs, c0, c1, end, mw, sw);
+        for (int p0 = 0; p0 < c1 - c0; p0 += q.na) {
+            const int p = p0 + q.rank;
+            const bool v = p < c1 - c0;
+            const int pr = v ? (int)qs->pair[p] : 0;
+            const int l = pr & 63;
+            Ray rr;
+            rr.o = shfl3(r.o, l);
+            rr.d = shfl3(r.d, l);
+            rr.inv = rr.d;  // not read by the primitive tests
+            const int cl = __shfl(cull, l);
+            if (v) {
+                double dist;
+                qs->res[p] = leaf_test(s, s.leaves[pr >> 6], rr, cl, dist) ? dist : -1.0;  // hits have dist >= 0 (or -0)
+            }
+        }
+        wave_lds_sync();
+        while (sr < end && sr < c1) {  // step 3, in this ray's leaf order
+            const int j = __builtin_ctzll(mr);
+            mr &= mr - 1;
+            const double d = qs->res[sr - c0];
+            if (!(d < 0.0) && (best.prim < 0 || best.dist > d)) {
+                best.dist = d;
+                best.prim = -1 - s.leaves[j].a;
+            }
+            ++sr;
+        }
+        wave_lds_sync();  // the next chunk reuses the slots
+    }
+}
+TPT_D Hit traverse_flat_c(const DScene& s, const Ray& r, int cull) {
+    Hit best;
+    best.prim = -1;
+    best.dist = 0.0;
+    int g0 = 0;
+    while (g0 < s.ngroup) {  // runs of flat groups, split at walk groups (the DFS order)
+        int g1 = g0;
+        while (g1 < s.ngroup && s.groups[g1].b >= 0) ++g1;
+        if (g1 > g0) flat_closest_c(s, g0, g1, r, cull, best);
+        if (g1 < s.ngroup) {
+            const DNode gn = s.groups[g1];
+            if (slab_hit_finite(gn.bmin[0], gn.bmin[1], gn.bmin[2], gn.bmax[0], gn.bmax[1], gn.bmax[2], r))
+                walk_group_closest(s, gn.a, r, cull, best);
+            ++g1;
+        }
+        g0 = g1;
+    }
+    return best;
+}
+// Shadow query (any hit with |hit - r.o|^2 < thr; r.o is the query's lc, see shadow_ray).
+TPT_D bool shadow_flat_c(const DScene& s, const Ray& r, double thr, int cull) {
+    uint64_t mask, any;
+    leaf_masks(s, 0, s.ngroup, r, true, mask, any);
+    bool sh = false;
+    if (any != 0) {
+        const QPlan q = q_plan(mask);
+        if (!q_compact_pays(s, q, any)) {
+            for (uint64_t m = any; m != 0; m &= m - 1) {
+                const int j = __builtin_ctzll(m);
+                if (((mask >> j) & 1) && !sh) {
+                    double dist;
+                    if (leaf_test(s, s.leaves[j], r, cull, dist)) {
+                        const V3 hx = r.o + mul(r.d, (float)dist);
+                        if (dot3(hx - r.o, hx - r.o) < thr) sh = true;
+                    }
+                }
+            }
+        } else {
+            QScratch* qs = wave_qs(s);
+            const int lane = (int)__lane_id();
+            qs->flag[lane] = 0u;
+            uint64_t mw = mask;
+            int sw = q.off;
+            const int end = q.off + q.cnt;
+            for (int c0 = 0; c0 < q.n; c0 += kQC) {
+                const int c1 = c0 + kQC < q.n ? c0 + kQC : q.n;
+                q_list(qs, c0, c1, end, mw, sw);
+                for (int p0 = 0; p0 < c1 - c0; p0 += q.na) {
+                    const int p = p0 + q.rank;
+                    const bool v = p < c1 - c0;
+                    const int pr = v ? (int)qs->pair[p] : 0;
+                    const int l = pr & 63;
+                    Ray rr;
+                    rr.o = shfl3(r.o, l);
+                    rr.d = shfl3(r.d, l);
+                    rr.inv = rr.d;
+                    const int cl = __shfl(cull, l);
+                    const double th = __shfl(thr, l);
+                    if (v) {
+                        double dist;
+                        if (leaf_test(s, s.leaves[pr >> 6], rr, cl, dist)) {
+                            const V3 hx = rr.o + mul(rr.d, (float)dist);
+                            if (dot3(hx - rr.o, hx - rr.o) < th) qs->flag[l] = 1u;
+                        }
+                    }
+                }
+                wave_lds_sync();  // the flags are final / the next chunk reuses the slots
+            }
+            sh = qs->flag[lane] != 0u;
+        }
+    }
+    for (int gi = 0; gi < s.ngroup; ++gi) {  // walk groups (any-hit: order is free)
+        const DNode gn = s.groups[gi];
+        if (gn.b >= 0) continue;
+        const bool pass =
+            !sh && slab_hit_finite(gn.bmin[0], gn.bmin[1], gn.bmin[2], gn.bmax[0], gn.bmax[1], gn.bmax[2], r);
+        if (pass) sh = walk_group_shadow(s, gn.a, r, r.o, thr, cull);
+    }
+    return sh;
+}
+
 TPT_D Hit traverse(const DScene& s, int root, const Ray& r, int cull) {
     const bool fin = wave_finite(r);
-    if (fin && root == 0 && (s.flat & kFlatHit)) return traverse_flat(s, r, cull);
+    if (fin && root == 0 && (s.flat & kFlatHit)) return s.qs ? traverse_flat_c(s, r, cull) : traverse_flat(s, r, cull);
     return fin ? traverse_t<true>(s, root, r, cull) : traverse_t<false>(s, root, r, cull);
 }
 
@@ -407,7 +646,7 @@ TPT_D bool shadow_ray(const DScene& s, V3 lc, V3 x, int cull) {
     if (!(thr > 0.0)) return false;  // d2 >= 0 can never be < thr (the lane leaves the wave's query)
     const Ray r = make_ray(lc, normalized(x - lc));
     const bool fin = wave_finite(r);
-    if (fin && (s.flat & kFlatShadow)) return shadow_flat(s, r, lc, thr, cull);
+    if (fin && (s.flat & kFlatShadow)) return s.qs ? shadow_flat_c(s, r, thr, cull) : shadow_flat(s, r, lc, thr, cull);
     return fin ? shadow_walk<true>(s, r, lc, thr, cull) : shadow_walk<false>(s, r, lc, thr, cull);
 }
 
