@@ -31,9 +31,13 @@ extern __shared__ __align__(16) unsigned char tpt_smem[];
 // the scene's node and triangle arrays are copied into LDS (16 B per lane per step)
 // and the kernel's DScene is pointed at them, so every traversal fetch is a ds_read
 // instead of a dependent L1/L2 load.  Returns the first LDS byte after the scene.
-template <bool kLds>
+// kSc: 0 no LDS (tree walks only), 1 LDS + a flat list of primitives only, 2 LDS + a
+// flat list with treelets or walk groups.  s.big is set to the constant kSc == 2 so
+// the compiler drops the large-scene branches from the small-scene kernels.
+template <int kSc>
 TPT_D unsigned char* stage_scene(DScene& s) {
-    if (!kLds) return tpt_smem;
+    s.big = kSc == 2;
+    if (kSc == 0) return tpt_smem;
     unsigned char* base = tpt_smem;
     const bool full = s.lds_full != 0;  // else only the flat-query arrays (+ ftris at the end)
     const int nb = full ? s.nnodes * (int)sizeof(DNode) : 0, tb = full ? s.ntri * (int)sizeof(DTri) : 0,
@@ -113,12 +117,12 @@ static_assert(kQ == 1 || kQ == 2 || kQ == 4 || kQ == 8 || kQ == 16, "Q must be a
 
 // kSeeded: TPT_FLAG_SAMPLE_SEED -- each sample seeds its own stream (sample_seed), so
 // no lane steps past the other lanes' samples.
-template <bool kLds, bool kSeeded>
+template <int kSc, bool kSeeded>
 __global__ __launch_bounds__(kBlock, TPT_PT_MINWAVES) void tpt_pt_kernel(DScene s, int spp, int64_t begin,
                                                                         int64_t stride, int64_t count,
                                                                         const int64_t* __restrict__ list,
                                                                         float* __restrict__ out) {
-    unsigned char* lds_free = stage_scene<kLds>(s);
+    unsigned char* lds_free = stage_scene<kSc>(s);
     s.qs = nullptr;  // coherent rays: the per-leaf flat loops (the compacted form's code folds away)
     V3 acc = v3s(0.0f);
     {
@@ -202,14 +206,22 @@ constexpr int kPtiMaxBounces = 1 << 16;
 // kSeeded (TPT_FLAG_SAMPLE_SEED): samples are independent, so kQ lanes share a pixel:
 // lane q runs samples q, q + kQ, ... back to back (each from sample_seed), sums its
 // own (1/spp) * L, and the kQ partial sums are added in lane order at the end.
-template <bool kLds, bool kSeeded>
+template <int kSc, bool kSeeded>
 __global__ __launch_bounds__(kBlock, TPT_PTI_MINWAVES) void tpt_pti_kernel(DScene s, int spp, int64_t begin,
                                                                           int64_t stride, int64_t count,
                                                                           const int64_t* __restrict__ list,
                                                                           float* __restrict__ out,
                                                                           unsigned long long* __restrict__ bounces) {
-    stage_scene<kLds>(s);
+    stage_scene<kSc>(s);
+#ifndef TPT_PTI_COMPACT
+#define TPT_PTI_COMPACT 1  // same-box A/B, Standard 1024 spp: 737 -> 708 ms
+#endif
+#if TPT_PTI_COMPACT
+    __shared__ QScratch qsm[kBlock / 64];  // incoherent bounce rays: compacted flat queries
+    s.qs = qsm;
+#else
     s.qs = nullptr;
+#endif
     constexpr int kL = kSeeded ? kQ : 1;  // lanes per pixel
     const int64_t gl = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     const int64_t k = gl / kL;
@@ -281,10 +293,10 @@ __global__ __launch_bounds__(kBlock, TPT_PTI_MINWAVES) void tpt_pti_kernel(DScen
 // efficiency).  Per-pixel order -- and so every RNG draw -- is unchanged.  Queues:
 // one counter per shard of pixels, shard = blockIdx.x % 8 (blocks b and b + 8 are
 // dealt to the same XCD; speed only).
-template <bool kLds>
+template <int kSc>
 __global__ __launch_bounds__(kBlock, TPT_GEN_MINWAVES) void tpt_bdpt_gen_kernel(DScene s, WfState w, int iter,
                                                                                unsigned* __restrict__ queue) {
-    stage_scene<kLds>(s);
+    stage_scene<kSc>(s);
     __shared__ QScratch qsm[kBlock / 64];  // compacted flat queries (tpt_device.h)
     s.qs = qsm;
     const int shard = blockIdx.x & 7;
@@ -412,9 +424,9 @@ __global__ __launch_bounds__(kBlock) void tpt_bdpt_scatter_kernel(WfState w, uns
 
 // One lane per strategy, grid-stride in wave-sized steps so that every lane of a
 // wave stays in the loop until the wave is done (splat_wave needs the whole wave).
-template <bool kLds>
+template <int kSc>
 __global__ __launch_bounds__(kBlock, TPT_CONN_MINWAVES) void tpt_bdpt_conn_kernel(DScene s, WfState w, float* __restrict__ splat) {
-    stage_scene<kLds>(s);
+    stage_scene<kSc>(s);
     __shared__ QScratch qsm[kBlock / 64];
     s.qs = qsm;
     const int64_t total = total_tasks(w);
@@ -526,6 +538,7 @@ struct tpt_ctx {
     unsigned long long* counters = nullptr;
     unsigned* queue = nullptr;  // persistent gen: 8 shard counters, 64 B apart
     int num_cu = 0;
+    int sc = 0;  // kernel scene class (stage_scene): 0 no LDS, 1 small flat scene, 2 flat + treelets / walk groups
     // wavefront BDPT state (sized for wf_cap pixels)
     void* wf_mem = nullptr;
     int64_t wf_cap = 0;
@@ -623,7 +636,6 @@ int64_t shard_count(int64_t npix, int64_t begin, int64_t stride) {
 // One BDPT wavefront over `count` (<= kWfChunk) pixel streams.
 int launch_bdpt_chunk(tpt_ctx* c, int spp, int64_t begin, int64_t stride, int64_t count, const int64_t* dlist,
                       float* drows, float* dsplat) {
-    const bool lds = c->ds.lds_bytes > 0;
     const size_t shmem = (size_t)c->ds.lds_bytes;
     // Two streams: gen/scan/scatter of iteration it on c->stream, connect/fold on
     // c->stream2, with the wavefront state double-buffered so gen(it+1) runs
@@ -640,10 +652,11 @@ int launch_bdpt_chunk(tpt_ctx* c, int spp, int64_t begin, int64_t stride, int64_
     const unsigned cblocks = (unsigned)std::min<int64_t>(TPT_CONN_GRID, (count * 24 + kBlock - 1) / kBlock + 1);
     // persistent gen grid: as many workgroups as are resident at once, a multiple of
     // the 8 queue shards, and no more than the pixels need
+    const auto gen_k = c->sc == 2 ? tpt_bdpt_gen_kernel<2> : c->sc == 1 ? tpt_bdpt_gen_kernel<1> : tpt_bdpt_gen_kernel<0>;
+    const auto conn_k = c->sc == 2 ? tpt_bdpt_conn_kernel<2> : c->sc == 1 ? tpt_bdpt_conn_kernel<1> : tpt_bdpt_conn_kernel<0>;
     int per_cu = 0;
     HIP_TRY(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                   &per_cu, lds ? (const void*)tpt_bdpt_gen_kernel<true> : (const void*)tpt_bdpt_gen_kernel<false>,
-                   kBlock, shmem));
+                   &per_cu, (const void*)gen_k, kBlock, shmem));
 #ifndef TPT_GEN_GRID_Q
 // gen's persistent grid, in 32nds of what fits on the chip at once.  A full grid
 // occupies every CU until the queue drains, so connect (other stream) only runs in
@@ -666,12 +679,7 @@ int launch_bdpt_chunk(tpt_ctx* c, int spp, int64_t begin, int64_t stride, int64_
         w.bounces = c->counters;
         if (it >= 2) HIP_TRY(c, hipStreamWaitEvent(c->stream, c->ev_fold[b], 0));
         if (it == 0) HIP_TRY(c, hipMemsetAsync(c->queue, 0, 8 * 64, c->stream));  // later: reset by scatter
-        if (lds)
-            hipLaunchKernelGGL(tpt_bdpt_gen_kernel<true>, dim3(gblocks), dim3(kBlock), shmem, c->stream, c->ds, w, it,
-                               c->queue);
-        else
-            hipLaunchKernelGGL(tpt_bdpt_gen_kernel<false>, dim3(gblocks), dim3(kBlock), shmem, c->stream, c->ds, w, it,
-                               c->queue);
+        hipLaunchKernelGGL(gen_k, dim3(gblocks), dim3(kBlock), shmem, c->stream, c->ds, w, it, c->queue);
         size_t bytes = c->scan_bytes;
         HIP_TRY(c, rocprim::inclusive_scan(c->scan_tmp, bytes, w.np, w.incl, (size_t)count,
                                            rocprim::plus<unsigned long long>(),
@@ -682,12 +690,7 @@ int launch_bdpt_chunk(tpt_ctx* c, int spp, int64_t begin, int64_t stride, int64_
         hipLaunchKernelGGL(tpt_bdpt_scatter_kernel, dim3(pblocks), dim3(kBlock), 0, c->stream, w, c->queue);
         HIP_TRY(c, hipEventRecord(c->ev_gen[b], c->stream));
         HIP_TRY(c, hipStreamWaitEvent(s2, c->ev_gen[b], 0));
-        if (lds)
-            hipLaunchKernelGGL(tpt_bdpt_conn_kernel<true>, dim3(cblocks), dim3(kBlock), shmem, s2, c->ds, w,
-                               dsplat);
-        else
-            hipLaunchKernelGGL(tpt_bdpt_conn_kernel<false>, dim3(cblocks), dim3(kBlock), shmem, s2, c->ds,
-                               w, dsplat);
+        hipLaunchKernelGGL(conn_k, dim3(cblocks), dim3(kBlock), shmem, s2, c->ds, w, dsplat);
         hipLaunchKernelGGL(tpt_bdpt_fold_kernel, dim3(pblocks), dim3(kBlock), 0, s2, w, inv);
         HIP_TRY(c, hipEventRecord(c->ev_fold[b], s2));
     }
@@ -712,19 +715,20 @@ int launch(tpt_ctx* c, int mode, int flags, int spp, int64_t begin, int64_t stri
     }
     HIP_TRY(c, hipMemsetAsync(c->counters, 0, sizeof(unsigned long long) * 32, c->stream));
     HIP_TRY(c, hipEventRecord(c->ev0, c->stream));
-    const bool lds = c->ds.lds_bytes > 0;
     const size_t shmem = (size_t)c->ds.lds_bytes;
     if (mode == TPT_MODE_PT) {
         const int64_t qblocks = (count * kQ + kBlock - 1) / kBlock;
         const size_t pshmem = shmem + (size_t)kPixSlots * kBlock * sizeof(float);
-        auto k = lds ? (seeded ? tpt_pt_kernel<true, true> : tpt_pt_kernel<true, false>)
-                     : (seeded ? tpt_pt_kernel<false, true> : tpt_pt_kernel<false, false>);
+        auto k = c->sc == 2   ? (seeded ? tpt_pt_kernel<2, true> : tpt_pt_kernel<2, false>)
+                 : c->sc == 1 ? (seeded ? tpt_pt_kernel<1, true> : tpt_pt_kernel<1, false>)
+                              : (seeded ? tpt_pt_kernel<0, true> : tpt_pt_kernel<0, false>);
         hipLaunchKernelGGL(k, dim3((unsigned)qblocks), dim3(kBlock), pshmem, c->stream, c->ds, spp, begin, stride,
                            count, dlist, drows);
     } else if (mode == TPT_MODE_PT_INDIRECT) {
         const int64_t lanes = count * (seeded ? kQ : 1);
-        auto k = lds ? (seeded ? tpt_pti_kernel<true, true> : tpt_pti_kernel<true, false>)
-                     : (seeded ? tpt_pti_kernel<false, true> : tpt_pti_kernel<false, false>);
+        auto k = c->sc == 2   ? (seeded ? tpt_pti_kernel<2, true> : tpt_pti_kernel<2, false>)
+                 : c->sc == 1 ? (seeded ? tpt_pti_kernel<1, true> : tpt_pti_kernel<1, false>)
+                              : (seeded ? tpt_pti_kernel<0, true> : tpt_pti_kernel<0, false>);
         hipLaunchKernelGGL(k, dim3((unsigned)((lanes + kBlock - 1) / kBlock)), dim3(kBlock), shmem, c->stream, c->ds,
                            spp, begin, stride, count, dlist, drows, c->counters);
     } else {
@@ -920,6 +924,9 @@ int tpt_upload_scene(tpt_ctx* c, const tpt_scene_desc* d) {
     const char* fl = std::getenv("TPT_FLAT");
     ds.flat = fl ? std::atoi(fl) : TPT_FLAT_DEFAULT;
     if (ds.nleaf > kFlatMaxLeaves || ds.lds_bytes == 0) ds.flat = 0;
+    ds.big = 0;
+    for (const DNode& g : hs.groups) ds.big |= g.b < 0;
+    c->sc = ds.lds_bytes == 0 ? 0 : ds.big ? 2 : 1;
     c->ds = ds;
     c->hs = std::move(hs);
     c->has_scene = true;

@@ -260,7 +260,7 @@ TPT_D Hit traverse_flat(const DScene& s, const Ray& r, int cull) {
         const DNode gn = s.groups[gi];
         const bool pass = slab_hit_finite(gn.bmin[0], gn.bmin[1], gn.bmin[2], gn.bmax[0], gn.bmax[1], gn.bmax[2], r);
         if (__ballot(pass) == 0) continue;
-        if (gn.b < 0) {
+        if (s.big && gn.b < 0) {
             if (pass) walk_group_closest(s, gn.a, r, cull, best);
             continue;
         }
@@ -290,7 +290,7 @@ TPT_D bool shadow_flat(const DScene& s, const Ray& r, V3 lc, double thr, int cul
         const bool pass =
             !sh && slab_hit_finite(gn.bmin[0], gn.bmin[1], gn.bmin[2], gn.bmax[0], gn.bmax[1], gn.bmax[2], r);
         if (__ballot(pass) == 0) continue;
-        if (gn.b < 0) {
+        if (s.big && gn.b < 0) {
             if (pass) sh = walk_group_shadow(s, gn.a, r, lc, thr, cull);
             continue;
         }
@@ -332,10 +332,17 @@ TPT_D bool shadow_flat(const DScene& s, const Ray& r, V3 lc, double thr, int cul
 // the same order: the result is the flat loop's, bit for bit.  A wave whose rays are
 // coherent (few leaves passed, by many lanes each) keeps the per-leaf loop; the
 // choice is made per wave and query.
-constexpr int kQC = 256;  // pair slots per chunk
+#ifndef TPT_QC
+#define TPT_QC 256
+#endif
+#ifndef TPT_QC_COST
+#define TPT_QC_COST 5  // a dense round costs about 5/4 of one wave-wide primitive test
+#endif
+constexpr int kQC = TPT_QC;  // pair slots per chunk
 struct QScratch {         // per wave, in LDS
     uint16_t pair[kQC];   // owner lane | leaf << 6
-    double res[kQC];      // closest hit: the pair's distance, -1 for no hit
+    double res[kQC];      // closest hit: the pair's nearest distance and primitive (-1: none)
+    int32_t prim[kQC];
     uint32_t flag[64];    // shadow query: the owner's ray is blocked
 };
 TPT_D QScratch* wave_qs(const DScene& s) { return reinterpret_cast<QScratch*>(s.qs) + (threadIdx.x >> 6); }
@@ -356,7 +363,7 @@ TPT_D void leaf_masks(const DScene& s, int g0, int g1, const Ray& r, bool on, ui
     any = 0;
     for (int gi = g0; gi < g1; ++gi) {
         const DNode gn = s.groups[gi];
-        if (gn.b < 0) continue;  // walk group: handled by the caller
+        if (s.big && gn.b < 0) continue;  // walk group: handled by the caller
         const bool pass = on && slab_hit_finite(gn.bmin[0], gn.bmin[1], gn.bmin[2], gn.bmax[0], gn.bmax[1], gn.bmax[2], r);
         if (__ballot(pass) == 0) continue;
         const int j1 = gn.a + gn.b;
@@ -392,7 +399,7 @@ TPT_D QPlan q_plan(uint64_t mask) {
 // Dense rounds beat one wave-wide test per passed leaf by a wide margin or not at all.
 TPT_D bool q_compact_pays(const DScene& s, const QPlan& q, uint64_t any) {
     const int rounds = (q.n + q.na - 1) / q.na;
-    return (s.flat & kFlatCompactAll) || (rounds + 1) * 5 < __popcll(any) * 4;
+    return (s.flat & kFlatCompactAll) || (rounds + 1) * TPT_QC_COST < __popcll(any) * 4;
 }
 // The primitive test of flat leaf n (as in traverse_flat / shadow_flat).
 TPT_D bool leaf_test(const DScene& s, const DNode& n, const Ray& r, int cull, double& dist) {
@@ -400,6 +407,22 @@ TPT_D bool leaf_test(const DScene& s, const DNode& n, const Ray& r, int cull, do
     if (prim < s.ntri) return tri_test(s.ftris[n.b], r, cull, dist);
     return sphere_test(s.sph[prim - s.ntri], r, cull, dist);
 }
+// Flat leaf n folded into `best` with BVHAccel::Intersect's strict `>` (BVH.cpp:103-143).
+TPT_D void entry_closest(const DScene& s, const DNode& n, const Ray& r, int cull, Hit& best) {
+    double dist;
+    if (leaf_test(s, n, r, cull, dist) && (best.prim < 0 || best.dist > dist)) {
+        best.dist = dist;
+        best.prim = -1 - n.a;
+    }
+}
+// Shadow answer of flat leaf n (a hit with |hit - r.o|^2 < thr).
+TPT_D bool entry_blocks(const DScene& s, const DNode& n, const Ray& r, double thr, int cull) {
+    double dist;
+    if (!leaf_test(s, n, r, cull, dist)) return false;
+    const V3 hx = r.o + mul(r.d, (float)dist);
+    return dot3(hx - r.o, hx - r.o) < thr;
+}
+
 TPT_D V3 shfl3(V3 a, int l) { return v3(__shfl(a.x, l), __shfl(a.y, l), __shfl(a.z, l)); }
 // Step 2a for the chunk of slots [c0, c1): each lane writes its pairs that fall in it
 // (mw / sw: its leaves and the slot of the next pair still to be listed).
@@ -424,19 +447,12 @@ TPT_D void flat_closest_c(const DScene& s, int g0, int g1, const Ray& r, int cul
     if (!q_compact_pays(s, q, any)) {
         for (uint64_t m = any; m != 0; m &= m - 1) {
             const int j = __builtin_ctzll(m);
-            if ((mask >> j) & 1) {
-                const DNode n = s.leaves[j];
-                double dist;
-                if (leaf_test(s, n, r, cull, dist) && (best.prim < 0 || best.dist > dist)) {
-                    best.dist = dist;
-                    best.prim = -1 - n.a;
-                }
-            }
+            if ((mask >> j) & 1) entry_closest(s, s.leaves[j], r, cull, best);
         }
         return;
     }
     QScratch* qs = wave_qs(s);
-    uint64_t mw = mask, mr = mask;
+    uint64_t mw = mask;
     int sw = q.off, sr = q.off;
     const int end = q.off + q.cnt;
     for (int c0 = 0; c0 < q.n; c0 += kQC) {
@@ -453,18 +469,21 @@ TPT_D void flat_closest_c(const DScene& s, int g0, int g1, const Ray& r, int cul
             rr.inv = rr.d;  // not read by the primitive tests
             const int cl = __shfl(cull, l);
             if (v) {
-                double dist;
-                qs->res[p] = leaf_test(s, s.leaves[pr >> 6], rr, cl, dist) ? dist : -1.0;  // hits have dist >= 0 (or -0)
+                Hit h;
+                h.prim = -1;
+                h.dist = 0.0;
+                entry_closest(s, s.leaves[pr >> 6], rr, cl, h);
+                qs->res[p] = h.dist;
+                qs->prim[p] = h.prim;
             }
         }
         wave_lds_sync();
         while (sr < end && sr < c1) {  // step 3, in this ray's leaf order
-            const int j = __builtin_ctzll(mr);
-            mr &= mr - 1;
             const double d = qs->res[sr - c0];
-            if (!(d < 0.0) && (best.prim < 0 || best.dist > d)) {
+            const int pp = qs->prim[sr - c0];
+            if (pp >= 0 && (best.prim < 0 || best.dist > d)) {
                 best.dist = d;
-                best.prim = -1 - s.leaves[j].a;
+                best.prim = pp;
             }
             ++sr;
         }
@@ -478,9 +497,9 @@ TPT_D Hit traverse_flat_c(const DScene& s, const Ray& r, int cull) {
     int g0 = 0;
     while (g0 < s.ngroup) {  // runs of flat groups, split at walk groups (the DFS order)
         int g1 = g0;
-        while (g1 < s.ngroup && s.groups[g1].b >= 0) ++g1;
+        while (g1 < s.ngroup && !(s.big && s.groups[g1].b < 0)) ++g1;
         if (g1 > g0) flat_closest_c(s, g0, g1, r, cull, best);
-        if (g1 < s.ngroup) {
+        if (g1 < s.ngroup) {  // a walk group
             const DNode gn = s.groups[g1];
             if (slab_hit_finite(gn.bmin[0], gn.bmin[1], gn.bmin[2], gn.bmax[0], gn.bmax[1], gn.bmax[2], r))
                 walk_group_closest(s, gn.a, r, cull, best);
@@ -500,13 +519,7 @@ TPT_D bool shadow_flat_c(const DScene& s, const Ray& r, double thr, int cull) {
         if (!q_compact_pays(s, q, any)) {
             for (uint64_t m = any; m != 0; m &= m - 1) {
                 const int j = __builtin_ctzll(m);
-                if (((mask >> j) & 1) && !sh) {
-                    double dist;
-                    if (leaf_test(s, s.leaves[j], r, cull, dist)) {
-                        const V3 hx = r.o + mul(r.d, (float)dist);
-                        if (dot3(hx - r.o, hx - r.o) < thr) sh = true;
-                    }
-                }
+                if (((mask >> j) & 1) && !sh) sh = entry_blocks(s, s.leaves[j], r, thr, cull);
             }
         } else {
             QScratch* qs = wave_qs(s);
@@ -529,20 +542,14 @@ TPT_D bool shadow_flat_c(const DScene& s, const Ray& r, double thr, int cull) {
                     rr.inv = rr.d;
                     const int cl = __shfl(cull, l);
                     const double th = __shfl(thr, l);
-                    if (v) {
-                        double dist;
-                        if (leaf_test(s, s.leaves[pr >> 6], rr, cl, dist)) {
-                            const V3 hx = rr.o + mul(rr.d, (float)dist);
-                            if (dot3(hx - rr.o, hx - rr.o) < th) qs->flag[l] = 1u;
-                        }
-                    }
+                    if (v && entry_blocks(s, s.leaves[pr >> 6], rr, th, cl)) qs->flag[l] = 1u;
                 }
                 wave_lds_sync();  // the flags are final / the next chunk reuses the slots
             }
             sh = qs->flag[lane] != 0u;
         }
     }
-    for (int gi = 0; gi < s.ngroup; ++gi) {  // walk groups (any-hit: order is free)
+    for (int gi = 0; s.big && gi < s.ngroup; ++gi) {  // walk groups (any-hit: order is free)
         const DNode gn = s.groups[gi];
         if (gn.b >= 0) continue;
         const bool pass =

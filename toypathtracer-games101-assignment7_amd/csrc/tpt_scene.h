@@ -123,6 +123,7 @@ struct DScene {
     int32_t nmats;
     int32_t lds_bytes;  // bytes staged in LDS per workgroup (0 = read from HBM/L2)
     int32_t lds_full;   // 1: nodes + triangles + flat arrays staged; 0: only the flat arrays
+    int32_t big;        // the flat list has walk groups (the kernels of small scenes fold it to 0)
     void* qs;           // device only: per-wave LDS scratch of the compacted flat queries (null: off)
 };
 
