@@ -100,31 +100,59 @@ TPT_D bool wave_finite(const Ray& r) { return __ballot(!ray_monotone(r)) == 0; }
 
 TPT_D V3 tri_normal(const DTri& t) { return v3(t.nx, t.ny, t.nz); }
 
+#ifndef TPT_TRI_BF
+#define TPT_TRI_BF 1  // tri_test's form in the per-lane walks and per-leaf loops (see below)
+#endif
+#ifndef TPT_TRI_BF_C
+#define TPT_TRI_BF_C 2  // ... and in the dense rounds of the compacted flat queries
+#endif
 // Triangle::GetIntersection (Triangle.cpp:77-118): culling on the f64 sign of
 // dot(d, n), then f64 Moller-Trumbore with |det| < EPSILON(1e-4f) rejection.
-TPT_D bool tri_test(const DTri t, const Ray& r, int cull, double& dist) {  // by value: all 48 B load up front
+// Every rejection returns the same `false` and every quantity is a pure function of
+// the ray and the triangle, so the tests may be evaluated in any order.
+template <int kBF>
+TPT_D bool tri_test_t(const DTri t, const Ray& r, int cull, double& dist) {  // by value: all 48 B load up front
     V3 n = tri_normal(t);
-    if (cull == TPT_CULL_BACK) {
-        if (dot3(r.d, n) > 0) return false;
-    } else if (cull == TPT_CULL_FRONT) {
-        if (dot3(r.d, n) < 0) return false;
+    if (kBF < 2) {
+        if (cull == TPT_CULL_BACK) {
+            if (dot3(r.d, n) > 0) return false;
+        } else if (cull == TPT_CULL_FRONT) {
+            if (dot3(r.d, n) < 0) return false;
+        }
     }
     V3 e1 = v3(t.e1[0], t.e1[1], t.e1[2]), e2 = v3(t.e2[0], t.e2[1], t.e2[2]);
     V3 pvec = cross(r.d, e2);
     double det = dot3(e1, pvec);
-    if (dabs_(det) < (double)1e-4f) return false;
-    double det_inv = 1. / det;
+    if (kBF < 2 && dabs_(det) < (double)1e-4f) return false;
     V3 tvec = r.o - v3(t.v0[0], t.v0[1], t.v0[2]);
-    double u = dot3(tvec, pvec) * det_inv;
-    if (u < 0 || u > 1) return false;
+    const double ua = dot3(tvec, pvec);
     V3 qvec = cross(tvec, e1);
-    double v = dot3(r.d, qvec) * det_inv;
-    if (v < 0 || u + v > 1) return false;
-    double tt = dot3(e2, qvec) * det_inv;
-    if (tt < 0.0f) return false;
+    const double vb = dot3(r.d, qvec);
+    double det_inv = 1. / det;
+    double u = ua * det_inv;
+    if (kBF == 0) {
+        if (u < 0 || u > 1) return false;
+        double v = vb * det_inv;
+        if (v < 0 || u + v > 1) return false;
+        double tt = dot3(e2, qvec) * det_inv;
+        if (tt < 0.0f) return false;
+        dist = tt;
+        return true;
+    }
+    // kBF >= 1: one predicate, the same comparisons (NaN passes each of them, as above);
+    // kBF == 2 folds the culling and |det| tests into it too (no branch at all)
+    const double v = vb * det_inv;
+    const double tt = dot3(e2, qvec) * det_inv;
+    bool rej = (u < 0) | (u > 1) | (v < 0) | (u + v > 1) | (tt < 0.0f);
+    if (kBF >= 2) {
+        const double dn = dot3(r.d, n);
+        rej = rej | (dabs_(det) < (double)1e-4f) | ((cull == TPT_CULL_BACK) & (dn > 0)) |
+              ((cull == TPT_CULL_FRONT) & (dn < 0));
+    }
     dist = tt;
-    return true;
+    return !rej;
 }
+TPT_D bool tri_test(const DTri t, const Ray& r, int cull, double& dist) { return tri_test_t<TPT_TRI_BF>(t, r, cull, dist); }
 
 // SolveQuadratic (SampleHelperFunctions.cpp:4-18), float parameters.
 TPT_D bool solve_quadratic(float a, float b, float c, float& x0, float& x1) {
@@ -402,23 +430,26 @@ TPT_D bool q_compact_pays(const DScene& s, const QPlan& q, uint64_t any) {
     return (s.flat & kFlatCompactAll) || (rounds + 1) * TPT_QC_COST < __popcll(any) * 4;
 }
 // The primitive test of flat leaf n (as in traverse_flat / shadow_flat).
+template <int kBF = TPT_TRI_BF>
 TPT_D bool leaf_test(const DScene& s, const DNode& n, const Ray& r, int cull, double& dist) {
     const int prim = -1 - n.a;
-    if (prim < s.ntri) return tri_test(s.ftris[n.b], r, cull, dist);
+    if (prim < s.ntri) return tri_test_t<kBF>(s.ftris[n.b], r, cull, dist);
     return sphere_test(s.sph[prim - s.ntri], r, cull, dist);
 }
 // Flat leaf n folded into `best` with BVHAccel::Intersect's strict `>` (BVH.cpp:103-143).
+template <int kBF = TPT_TRI_BF>
 TPT_D void entry_closest(const DScene& s, const DNode& n, const Ray& r, int cull, Hit& best) {
     double dist;
-    if (leaf_test(s, n, r, cull, dist) && (best.prim < 0 || best.dist > dist)) {
+    if (leaf_test<kBF>(s, n, r, cull, dist) && (best.prim < 0 || best.dist > dist)) {
         best.dist = dist;
         best.prim = -1 - n.a;
     }
 }
 // Shadow answer of flat leaf n (a hit with |hit - r.o|^2 < thr).
+template <int kBF = TPT_TRI_BF>
 TPT_D bool entry_blocks(const DScene& s, const DNode& n, const Ray& r, double thr, int cull) {
     double dist;
-    if (!leaf_test(s, n, r, cull, dist)) return false;
+    if (!leaf_test<kBF>(s, n, r, cull, dist)) return false;
     const V3 hx = r.o + mul(r.d, (float)dist);
     return dot3(hx - r.o, hx - r.o) < thr;
 }
@@ -472,7 +503,7 @@ TPT_D void flat_closest_c(const DScene& s, int g0, int g1, const Ray& r, int cul
                 Hit h;
                 h.prim = -1;
                 h.dist = 0.0;
-                entry_closest(s, s.leaves[pr >> 6], rr, cl, h);
+                entry_closest<TPT_TRI_BF_C>(s, s.leaves[pr >> 6], rr, cl, h);
                 qs->res[p] = h.dist;
                 qs->prim[p] = h.prim;
             }
@@ -542,7 +573,7 @@ TPT_D bool shadow_flat_c(const DScene& s, const Ray& r, double thr, int cull) {
                     rr.inv = rr.d;
                     const int cl = __shfl(cull, l);
                     const double th = __shfl(thr, l);
-                    if (v && entry_blocks(s, s.leaves[pr >> 6], rr, th, cl)) qs->flag[l] = 1u;
+                    if (v && entry_blocks<TPT_TRI_BF_C>(s, s.leaves[pr >> 6], rr, th, cl)) qs->flag[l] = 1u;
                 }
                 wave_lds_sync();  // the flags are final / the next chunk reuses the slots
             }
