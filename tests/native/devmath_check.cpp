@@ -95,5 +95,14 @@ int main(int argc, char** argv) {
         }
     }
     printf("div3_rcp n=%ld bad=%ld\n", n6, bad6);
-    return (bad || bad2 || bad3 || bad4 || bad5 || bad6) ? 1 : 0;
+    // the integer coin of the PT stream skip: rng_float >= 0.5f <=> x >= kCoinHalf,
+    // every 32-bit output (stride ignored: an integer compare and one product each)
+    long bad7 = 0, n7 = 0;
+    for (uint64_t x = 0; x <= 0xffffffffull; ++x) {
+        const bool a = (float)((double)(uint32_t)x * (1.0 / 4294967295.0)) >= 0.5f;
+        n7++;
+        if (a != ((uint32_t)x >= kCoinHalf)) bad7++;
+    }
+    printf("coin n=%ld bad=%ld\n", n7, bad7);
+    return (bad || bad2 || bad3 || bad4 || bad5 || bad6 || bad7) ? 1 : 0;
 }

@@ -100,7 +100,7 @@ TPT_D uint32_t skip_samples(uint32_t st, int type, int light_draws, int n) {
         xorshift32(st);
         xorshift32(st);
         if (type == TPT_DIELETRIC) {
-            if (rng_float(st) >= 0.5f) { xorshift32(st); xorshift32(st); }
+            if (xorshift32(st) >= kCoinHalf) { xorshift32(st); xorshift32(st); }  // rng_float(st) >= 0.5f
         } else if (type == TPT_TRANSPARENT) {
             xorshift32(st);
         }

@@ -327,7 +327,7 @@ TPT_D bool shadow_flat(const DScene& s, const Ray& r, V3 lc, double thr, int cul
             const DNode n = s.leaves[j];
             if (!sh && slab_hit_finite(n.bmin[0], n.bmin[1], n.bmin[2], n.bmax[0], n.bmax[1], n.bmax[2], r)) {
                 const int prim = -1 - n.a;
-                double dist;
+                double dist = 0.0;
                 bool h;
                 if (prim < s.ntri) h = tri_test(s.ftris[n.b], r, cull, dist);
                 else h = sphere_test(s.sph[prim - s.ntri], r, cull, dist);
@@ -448,7 +448,7 @@ TPT_D void entry_closest(const DScene& s, const DNode& n, const Ray& r, int cull
 // Shadow answer of flat leaf n (a hit with |hit - r.o|^2 < thr).
 template <int kBF = TPT_TRI_BF>
 TPT_D bool entry_blocks(const DScene& s, const DNode& n, const Ray& r, double thr, int cull) {
-    double dist;
+    double dist = 0.0;
     if (!leaf_test<kBF>(s, n, r, cull, dist)) return false;
     const V3 hx = r.o + mul(r.d, (float)dist);
     return dot3(hx - r.o, hx - r.o) < thr;
@@ -1010,7 +1010,7 @@ TPT_D V3 mat_sample(const Mat& m, V3 wo, const Shade& sh, float* pdf, uint32_t& 
         return wis;
     }
     if (m.type == TPT_DIELETRIC) {
-        if (rng_float(rs) < 0.5f) {
+        if (xorshift32(rs) < kCoinHalf) {  // rng_float(rs) < 0.5f
             float pd = cosine_pdf(n, wis);
             *pdf = (pdf_h * jr + pd) * 0.5f;
             if ((double)vn * dot3(wis, n) < 0.0f) *pdf = 0.0f;

@@ -140,6 +140,10 @@ TPT_HD uint32_t xorshift32(uint32_t& s) {
 TPT_HD float rng_float(uint32_t& s) {
     return (float)((double)xorshift32(s) * (1.0 / 4294967295.0));
 }
+// rng_float is non-decreasing in the XorShift32 output x, so rng_float(s) >= 0.5f
+// exactly when x >= kCoinHalf, the smallest x whose float is 0.5f (x = kCoinHalf - 1
+// gives 0.49999997f; tests/native/devmath_check.cpp checks all 2^32 outputs).
+constexpr uint32_t kCoinHalf = 0x7fffffc0u;
 // TPT_FLAG_SAMPLE_SEED (include/tpt.h): sample j of pixel i starts its own stream.
 // SplitMix64's finalizer of ((i + 1) << 32 | j), folded to 32 bits, never 0
 // (a zero XorShift32 state stays zero).  Not the reference's seeding.
