@@ -77,6 +77,9 @@ TPT_D unsigned char* stage_scene(DScene& s) {
     return base + s.lds_bytes;
 }
 
+#ifndef TPT_PT_JUMP
+#define TPT_PT_JUMP 1  // jump tables for the PT stream skip (see build_jump)
+#endif
 #ifndef TPT_PT_MINWAVES
 #define TPT_PT_MINWAVES 5  // waves per SIMD the PT kernel's register budget must allow (measured: 4 / 5 / 6 = 52.9 / 50.8 / 57.1 ms; 5 spills 112 B/lane and still wins)
 #endif
@@ -109,6 +112,47 @@ TPT_D uint32_t skip_samples(uint32_t st, int type, int light_draws, int n) {
     return st;
 }
 
+// Jump tables for the stream skip of a Dieletric or Transparent camera hit.  XorShift32
+// is linear over GF(2)^32, so n steps map x to XOR_k T_n[k][byte k of x] with
+// T_n[k][b] = the state n steps from b << 8k.  A skipped Dieletric sample draws 3 + L
+// numbers, 2 more when its coin (the 3rd) is >= 0.5 (skip_samples), so from one
+// sample's coin state the next sample's coin state is L + 3 or L + 5 steps away: one
+// table jump per skipped sample instead of 5-7 XorShift steps (a Transparent sample
+// always draws 3 + L).  Word [k][b][far] of the table (8 KB of LDS): far = 0 for
+// L + 3 steps, 1 for L + 5.
+constexpr int kJumpWords = 4 * 256 * 2;
+constexpr size_t kLdsGranule = 1280;  // LDS allocation unit (measured, see launch())
+TPT_D void build_jump(uint32_t* jt, int light_draws) {
+    for (int e = threadIdx.x; e < 4 * 256; e += kBlock) {
+        uint32_t x = (uint32_t)(e & 255) << (8 * (e >> 8));
+        for (int i = 0; i < light_draws + 3; ++i) xorshift32(x);
+        jt[2 * e] = x;
+        xorshift32(x);
+        xorshift32(x);
+        jt[2 * e + 1] = x;
+    }
+}
+TPT_D uint32_t jump(const uint32_t* jt, uint32_t x, bool coin) {
+    const uint32_t far = coin && x >= kCoinHalf ? 1u : 0u;  // a Dieletric coin: rng_float(x) >= 0.5f
+    return jt[(x & 255u) << 1 | far] ^ jt[512 + ((x >> 8 & 255u) << 1 | far)] ^
+           jt[1024 + ((x >> 16 & 255u) << 1 | far)] ^ jt[1536 + ((x >> 24) << 1 | far)];
+}
+// skip_samples through the jump table, n >= 1 samples, for a Dieletric hit (the chain
+// runs over the skipped samples' coin states) or a Transparent one (3 + L draws per
+// sample, always: the chain runs over sample starts with far = 0).
+TPT_D uint32_t skip_jump(uint32_t st, const uint32_t* jt, int light_draws, int n, bool diel) {
+    if (diel) {
+        xorshift32(st);
+        xorshift32(st);
+        xorshift32(st);  // the first skipped sample's coin state
+    }
+    for (int j = 1; j < n; ++j) st = jump(jt, st, diel);
+    if (!diel) return jump(jt, st, false);
+    if (st >= kCoinHalf) { xorshift32(st); xorshift32(st); }
+    for (int d = 0; d < light_draws; ++d) xorshift32(st);
+    return st;
+}
+
 #ifndef TPT_PT_LANES
 #define TPT_PT_LANES 8  // Q lanes per PT pixel stream (1, 2, 4, 8 or 16; 8 measured best on one MI355X)
 #endif
@@ -121,8 +165,13 @@ template <int kSc, bool kSeeded>
 __global__ __launch_bounds__(kBlock, TPT_PT_MINWAVES) void tpt_pt_kernel(DScene s, int spp, int64_t begin,
                                                                         int64_t stride, int64_t count,
                                                                         const int64_t* __restrict__ list,
-                                                                        float* __restrict__ out) {
+                                                                        float* __restrict__ out, int use_jump) {
     unsigned char* lds_free = stage_scene<kSc>(s);
+    uint32_t* jt = reinterpret_cast<uint32_t*>(lds_free + kPixSlots * kBlock * sizeof(float));
+    if (!kSeeded && kQ > 2 && use_jump) {
+        build_jump(jt, s.light_draws);
+        __syncthreads();
+    }
     s.qs = nullptr;  // coherent rays: the per-leaf flat loops (the compacted form's code folds away)
     V3 acc = v3s(0.0f);
     {
@@ -158,7 +207,12 @@ __global__ __launch_bounds__(kBlock, TPT_PT_MINWAVES) void tpt_pt_kernel(DScene 
                         rs = sample_seed(list ? list[kk] : begin + kk * stride, j0 + qq);
                     }
                     L = mul(pt_sample(s, px, rs), inv);
-                    if (kQ > 1 && !kSeeded) rs = skip_samples(rs, px.type(), s.light_draws, kQ - 1);
+                    if (kQ > 1 && !kSeeded) {
+                        const int ty = px.type();
+                        rs = kQ > 2 && use_jump && ty != TPT_METAL
+                                 ? skip_jump(rs, jt, s.light_draws, kQ - 1, ty == TPT_DIELETRIC)
+                                 : skip_samples(rs, ty, s.light_draws, kQ - 1);
+                    }
                 }
                 if (kQ == 1) {
                     acc = acc + L;
@@ -718,12 +772,17 @@ int launch(tpt_ctx* c, int mode, int flags, int spp, int64_t begin, int64_t stri
     const size_t shmem = (size_t)c->ds.lds_bytes;
     if (mode == TPT_MODE_PT) {
         const int64_t qblocks = (count * kQ + kBlock - 1) / kBlock;
-        const size_t pshmem = shmem + (size_t)kPixSlots * kBlock * sizeof(float);
+        size_t pshmem = shmem + (size_t)kPixSlots * kBlock * sizeof(float);
+        // The jump table only where the workgroup still fits 5 times (TPT_PT_MINWAVES) in a
+        // CU's LDS.  Measured: 31,872 B per workgroup keeps 5 resident, 32,128 B does not
+        // (46.4 vs 49.9 ms, Standard); consistent with 1,280-B allocation granules in 160 KB.
+        const int use_jump = !seeded && TPT_PT_JUMP && pshmem + kJumpWords * 4 <= kLdsGranule * (160 * 1024 / kLdsGranule / TPT_PT_MINWAVES);
+        if (use_jump) pshmem += kJumpWords * 4;
         auto k = c->sc == 2   ? (seeded ? tpt_pt_kernel<2, true> : tpt_pt_kernel<2, false>)
                  : c->sc == 1 ? (seeded ? tpt_pt_kernel<1, true> : tpt_pt_kernel<1, false>)
                               : (seeded ? tpt_pt_kernel<0, true> : tpt_pt_kernel<0, false>);
         hipLaunchKernelGGL(k, dim3((unsigned)qblocks), dim3(kBlock), pshmem, c->stream, c->ds, spp, begin, stride,
-                           count, dlist, drows);
+                           count, dlist, drows, use_jump);
     } else if (mode == TPT_MODE_PT_INDIRECT) {
         const int64_t lanes = count * (seeded ? kQ : 1);
         auto k = c->sc == 2   ? (seeded ? tpt_pti_kernel<2, true> : tpt_pti_kernel<2, false>)
