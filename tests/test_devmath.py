@@ -4,6 +4,8 @@ glibc, compiled as host code.  Stride 1 = exhaustive (every float of each domain
 import os
 import subprocess
 
+import pytest
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
@@ -17,3 +19,13 @@ def test_devmath_matches_glibc(tmp_path):
     assert r.returncode == 0, r.stdout
     for line in r.stdout.strip().splitlines():
         assert line.endswith("bad=0"), line
+
+
+@pytest.mark.gpu
+def test_fast_reciprocal_exhaustive():
+    """rcp_fast_f32 (make_ray's 1/d) equals IEEE 1.0f / x for every float it is used on."""
+    exe = os.path.join(ROOT, "tests", "native", "build", "rcpf_check")
+    assert os.path.exists(exe), "built by __graft_entry__.build()"
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+    print(r.stdout)
+    assert r.returncode == 0, r.stdout + r.stderr

@@ -28,10 +28,21 @@ struct Ray {
 // operation on floats carried out in double and rounded to float equals the
 // correctly rounded float operation (double rounding is innocuous since
 // 53 >= 2*24 + 2), so the exact f32 divide is used.
+#ifndef TPT_FAST_RCP
+#define TPT_FAST_RCP 1
+#endif
 TPT_D Ray make_ray(V3 o, V3 d) {
     Ray r;
     r.o = o;
     r.d = d;
+#if TPT_FAST_RCP
+    // rcp_fast_f32 equals the IEEE quotient on its range (tpt_devmath.h); a wave with a
+    // component outside it (0, denormal, huge: rare) divides.
+    if (__ballot(!(rcp_fast_ok(d.x) & rcp_fast_ok(d.y) & rcp_fast_ok(d.z))) == 0) {
+        r.inv = v3(rcp_fast_f32(d.x), rcp_fast_f32(d.y), rcp_fast_f32(d.z));
+        return r;
+    }
+#endif
     r.inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
     return r;
 }

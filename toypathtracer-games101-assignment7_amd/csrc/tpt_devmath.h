@@ -89,6 +89,21 @@ TPT_HD V3 divs(V3 a, float r) {  // Vector.hpp:26
     return v3(a.x / r, a.y / r, a.z / r);
 }
 
+// 1.0f / x from v_rcp_f32 and one Newton correction (e = 1 - x*y exactly by fma,
+// y + e*y): equal to the IEEE quotient for every x with 2^-126 <= |x| <= 2^126
+// (rcp_fast_ok), checked on the GPU over all 2^32 floats (tests/native/rcpf_check.hip).
+#if defined(__HIPCC__)
+__device__ __forceinline__ float rcp_fast_f32(float x) {
+    const float y = __builtin_amdgcn_rcpf(x);
+    const float e = __builtin_fmaf(-x, y, 1.0f);
+    return __builtin_fmaf(e, y, y);
+}
+#endif
+TPT_HD bool rcp_fast_ok(float x) {
+    const float a = fabs_(x);
+    return a >= 1.17549435e-38f && a <= 8.50705917e+37f;  // [2^-126, 2^126]
+}
+
 // Vector.hpp:103-104 (see header note on the fma form)
 TPT_HD double dot3(V3 a, V3 b) {
 #if defined(__HIPCC__) && defined(__HIP_DEVICE_COMPILE__)
