@@ -159,6 +159,27 @@ TPT_D uint32_t skip_jump(uint32_t st, const uint32_t* jt, int light_draws, int n
 constexpr int kQ = TPT_PT_LANES;
 static_assert(kQ == 1 || kQ == 2 || kQ == 4 || kQ == 8 || kQ == 16, "Q must be a power of two dividing the wave");
 
+#ifndef TPT_PT_DPP
+#define TPT_PT_DPP 1
+#endif
+// acc += L of lane (this + jj) for jj = J, J + 1, ... < n (n <= 8), in that order.
+template <int J>
+TPT_D void fold_dpp(V3& acc, V3 L, int n) {
+    if constexpr (J < 8) {
+        if (J < n) {
+            if (J == 0) {
+                acc = acc + L;
+            } else {
+                constexpr int ctrl = 0x100 + J;  // DPP row_shl:J
+                acc.x = acc.x + __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, L.x), ctrl, 0xf, 0xf, false));
+                acc.y = acc.y + __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, L.y), ctrl, 0xf, 0xf, false));
+                acc.z = acc.z + __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, L.z), ctrl, 0xf, 0xf, false));
+            }
+            fold_dpp<J + 1>(acc, L, n);
+        }
+    }
+}
+
 // kSeeded: TPT_FLAG_SAMPLE_SEED -- each sample seeds its own stream (sample_seed), so
 // no lane steps past the other lanes' samples.
 template <int kSc, bool kSeeded>
@@ -216,6 +237,12 @@ __global__ __launch_bounds__(kBlock, TPT_PT_MINWAVES) void tpt_pt_kernel(DScene 
                 }
                 if (kQ == 1) {
                     acc = acc + L;
+                } else if (kQ == 8 && TPT_PT_DPP) {
+                    // The fold through DPP row shifts: lane i reads L of lane i + jj of its
+                    // 16-lane row, so the first lane of each pixel (i = 0 mod 8) adds its
+                    // pixel's samples in sample order (other lanes' acc is never read).
+                    const int n = spp - j0 < kQ ? spp - j0 : kQ;
+                    fold_dpp<0>(acc, L, n);
                 } else {
                     const int base = (int)(ln & 63) - qq;  // first lane of this pixel
                     const int n = spp - j0 < kQ ? spp - j0 : kQ;
