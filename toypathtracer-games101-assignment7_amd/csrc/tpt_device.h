@@ -946,13 +946,15 @@ TPT_D float mat_pdf(const Mat& m, V3 wo, V3 n, V3 wi) { return mat_pdf(m, wo, ma
 // even in its argument, so GGXTerm(|n.h|) == GGXTerm(n.h)), v.h and l.h; only the
 // Fresnel argument differs (evalGivenSample uses fresnel(wi, h), pdf uses
 // fresnel(wo, h): Material.cpp:24 vs :112).  Same float ops as the two functions.
-TPT_D void bsdf_pdf(const Mat& m, V3 wo, V3 wi, V3 N, V3& f_out, float& pdf_out) {
+// kCos: evalGivenSample with combineCosineTerm = true (PathTrace's light branch);
+// nv = (float)DotProduct(N, wo) as the caller has it (the Shade).
+template <bool kCos>
+TPT_D void bsdf_pdf_t(const Mat& m, V3 wo, V3 wi, V3 N, float nv, V3& f_out, float& pdf_out) {
     f_out = v3s(0.0f);
     pdf_out = 0.0f;
     float nl = (float)dot3(N, wi);
-    float nv = (float)dot3(N, wo);
     if (nl == 0.0f || nv == 0.0f) return;
-    V3 h = half_dir(N, wi, wo, m.ior_d);
+    V3 h = half_dir(N, wi, wo, nv, m.ior_d);
     const double dnh = dot3(N, h);
     float nh = (float)dnh;
     float lh = (float)dot3(wi, h);
@@ -965,7 +967,7 @@ TPT_D void bsdf_pdf(const Mat& m, V3 wo, V3 wi, V3 N, V3& f_out, float& pdf_out)
         float pdf_h = (float)((double)D * d);  // ggx_half_pdf
         float avh = fabs_(vh);
         float ior_i, ior_o;
-        inout_ior(N, wi, wo, m.ior_d, ior_i, ior_o);
+        inout_ior(N, wi, nv, m.ior_d, ior_i, ior_o);
         if (nv * nl < 0.0f) {
             float den = ior_i * lh + ior_o * vh;
             float jac = safe_div(ior_o * ior_o * avh, den * den);
@@ -978,17 +980,20 @@ TPT_D void bsdf_pdf(const Mat& m, V3 wo, V3 wi, V3 N, V3& f_out, float& pdf_out)
             else pdf_out = pdf_h * fp.x * jac;
         }
     }
-    // ---- Material::evalGivenSample, combineCosineTerm = false (Material.cpp:11-72)
+    // ---- Material::evalGivenSample (Material.cpp:11-72)
     float G = ggx_vis(nv, vh, m.rough) * ggx_vis(nl, lh, m.rough);
     V3 f = fresnel(m, wi, h);
     if (nl * nv > 0.0f) {
         V3 spec = v3s(0.0f);
         if (G != 0.0f) {
             spec = divs(mul(mul(f, D), G), (float)(4.0 * (double)fabs_(nv)));
-            spec = divs(spec, fabs_(nl));
+            if (!kCos) spec = divs(spec, fabs_(nl));
         }
         V3 diff = v3s(0.0f);
-        if (m.type == TPT_DIELETRIC) diff = divs(m.kd * (v3s(1.0f) - f), kPi);
+        if (m.type == TPT_DIELETRIC) {
+            diff = divs(m.kd * (v3s(1.0f) - f), kPi);
+            if (kCos) diff = mul(diff, saturate(nl));
+        }
         f_out = diff + spec;
         return;
     }
@@ -997,12 +1002,16 @@ TPT_D void bsdf_pdf(const Mat& m, V3 wo, V3 wi, V3 N, V3& f_out, float& pdf_out)
     if (nv < 0.0f) { ior_i = 1.0f; ior_o = m.ior_d; }
     else { ior_i = m.ior_d; ior_o = 1.0f; }
     float pa = fabs_(vh) * fabs_(lh) / (fabs_(nv));
-    pa /= fabs_(nl);
+    if (!kCos) pa /= fabs_(nl);
     float pb = ior_o * ior_o * (1.0f - f.x) * G * D;
     if (pa * pb == 0.0f) return;
     float pc = ior_i * lh + ior_o * vh;
     pc *= pc;
     f_out = v3s(pa * pb / pc);
+}
+
+TPT_D void bsdf_pdf(const Mat& m, V3 wo, V3 wi, V3 N, V3& f_out, float& pdf_out) {
+    bsdf_pdf_t<false>(m, wo, wi, N, (float)dot3(N, wo), f_out, pdf_out);
 }
 
 // Material::sample (Material.cpp:150-214)
@@ -1281,15 +1290,20 @@ TPT_D V3 pt_sample(const DScene& s, PixPark px, uint32_t& rs) {
             }
         }
         // the light branch (PathTracer.cpp:95-106); plb is pure, so it is computed here
-        float plb = mat_pdf(px.mat(s), px.v(kPxWo), px.shade(), wil);
+        // Material::pdf and evalGivenSample(.., true) of wil together (one half vector)
+        float plb;
+        V3 fl;
+        {
+            const Shade sh = px.shade();
+            bsdf_pdf_t<true>(px.mat(s), px.v(kPxWo), wil, sh.n, sh.nv, fl, plb);
+        }
         if (pll + plb > 0.0f) {
             Ray rl = make_ray(px.v(kPxX), wil);
             Hit hl = object_hit(s, o, rl, TPT_CULL_BACK);
             V3 hx = v3s(0.0f), hn;  // default Intersection::coords when missed (Intersection.hpp:14-21)
             if (hl.prim >= 0) hit_geometry(s, rl, hl, hx, hn);
             const bool sh = shadow_ray(s, hx, px.v(kPxX), TPT_CULL_BACK);
-            if (!sh)
-                ev = ev + divs(eval_bsdf(px.mat(s), px.v(kPxWo), wil, px.shade(), true), 1e-4f + pll + plb);
+            if (!sh) ev = ev + divs(fl, 1e-4f + pll + plb);
         }
         result = result + ev * load_mat(s, o.mat).em;
     }
