@@ -255,13 +255,17 @@ class Runner:
         stream = torch.cuda.current_stream()
         flags = pytpt.FLAG_SAMPLE_SEED if (self.args.sample_seed and self.args.mode in ("pt", "pti")) else 0
 
+        # PT modes write no splats (PathTrace has no light-tracing strategy), so only the
+        # rgb half of the buffer is summed; BDPT sums rgb and splat in one reduce.
+        red = fb if mode == "bdpt" else fb[:1]
+
         def step():
             # libtpt renders on its own stream: everything torch's stream has queued on
             # fb (the zero fill, the previous step's reduce) must finish before it
             # rewrites the buffers.
             stream.synchronize()
             st = self.ctx.render_device(spp, m, fb[0].data_ptr(), fb[1].data_ptr(), begin, stride, flags)
-            self.sharding.reduce_frame(self.dist, fb, dst=0)  # rgb + splat onto rank 0 (RCCL over xGMI)
+            self.sharding.reduce_frame(self.dist, red, dst=0)  # onto rank 0 (RCCL over xGMI)
             return st
 
         for _ in range(warmup):

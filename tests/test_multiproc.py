@@ -44,7 +44,8 @@ def _worker(rank, world, port, mode, spp, out_path):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     import sharding
     fb = torch.from_numpy(_render_shard(rank, world, mode, spp))
-    sharding.reduce_frame(dist, fb, dst=0)
+    # as bench.py: PT splats nothing, so only the rgb row is summed; BDPT sums both
+    sharding.reduce_frame(dist, fb if mode == 1 else fb[:1], dst=0)
     if rank == 0:
         np.save(out_path, fb.numpy())
     dist.destroy_process_group()

@@ -27,8 +27,9 @@ def shard_pixels(npix, rank, world):
 
 
 def reduce_frame(dist, fb, dst=0):
-    """Sum the rank-local framebuffer(s) `fb` (one tensor: [2, H*W*3] rgb + splat)
-    onto `dst` with a single collective."""
+    """Sum the rank-local framebuffer(s) `fb` (one contiguous tensor: [2, H*W*3] rgb +
+    splat for BDPT, the [1, H*W*3] rgb row for PT, which splats nothing) onto `dst`
+    with a single collective."""
     if dist is not None and dist.is_initialized() and dist.get_world_size() > 1:
         dist.reduce(fb, dst=dst)
     return fb
