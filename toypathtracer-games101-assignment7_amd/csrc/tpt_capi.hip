@@ -229,7 +229,7 @@ __global__ __launch_bounds__(kBlock, TPT_PT_MINWAVES) void tpt_pt_kernel(DScene 
                     }
                     L = mul(pt_sample(s, px, rs), inv);
                     if (kQ > 1 && !kSeeded) {
-                        const int ty = px.type();
+                        const int ty = px.type(s);
                         rs = kQ > 2 && use_jump && ty != TPT_METAL
                                  ? skip_jump(rs, jt, s.light_draws, kQ - 1, ty == TPT_DIELETRIC)
                                  : skip_samples(rs, ty, s.light_draws, kQ - 1);

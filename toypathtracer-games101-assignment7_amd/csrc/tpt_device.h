@@ -1170,8 +1170,7 @@ TPT_D Hit object_hit(const DScene& s, const DObj& o, const Ray& r, int cull) {
 // of 18) they made the occlusion and refractive-ball scenes 7 % slower and Standard
 // 0.3 % faster (same-box A/B: 47.6 / 54.7 / 50.6 ms vs 44.2 / 51.0 / 50.8 ms).
 enum PixSlot {
-    kPxMat = 0,
-    kPxType,
+    kPxMat = 0,  // the material type is read from the LDS material table by this index
     kPxX,
     kPxN = kPxX + 3,
     kPxWo = kPxN + 3,
@@ -1192,7 +1191,7 @@ struct PixPark {
         return v3(p[k * kBlock], p[(k + 1) * kBlock], p[(k + 2) * kBlock]);
     }
     TPT_D int mat_index() const { return __float_as_int(lane()[kPxMat * kBlock]); }
-    TPT_D int type() const { return __float_as_int(lane()[kPxType * kBlock]); }
+    TPT_D int type(const DScene& s) const { return s.mats[mat_index()].type; }
     TPT_D Shade shade() const {
         Shade f;
         f.n = v(kPxN);
@@ -1204,7 +1203,7 @@ struct PixPark {
     TPT_D Mat mat(const DScene& s) const {
         const DMat& d = s.mats[mat_index()];
         Mat m;
-        m.type = type();
+        m.type = d.type;
         m.ior_d = d.ior_d;
         m.rough = d.rough;
         const float* kdm = m.type == TPT_METAL ? d.ior_m : d.kd;  // each type reads only its own
@@ -1222,7 +1221,6 @@ struct PixPark {
     }
     TPT_D void park(V3 x, V3 n, V3 wo, int mi, const Mat& m) {
         put(kPxMat, __int_as_float(mi));
-        put(kPxType, __int_as_float(m.type));
         put3(kPxX, x);
         put3(kPxN, n);
         put3(kPxWo, wo);
