@@ -23,14 +23,18 @@ for w in pt bdpt c5 pti; do
     done; } > "profiles/${tag}_${w}_pmc.txt"
 done
 src_of() { echo "profiles/${tag}_$1_pmc.txt, profiles/${tag}_valu_cost.jsonl"; }
-python3 scripts/valu_model.py "$p" standard/pt pt tpt_pt_kernel --frames 2 --samples 629407744 \
-    --note "build $build" --source "$(src_of pt)" > /dev/null
-python3 scripts/pmc_traffic.py standard/pt tpt_pt_kernel "$p/pt_fetch/run_counter_collection.csv" \
-    "$p/pt_write/run_counter_collection.csv" --frames 2 --note "build $build (profiles/${tag}_pt_pmc.txt)" > /dev/null
-python3 scripts/valu_model.py "$p" standard/bdpt bdpt tpt_bdpt_ --scale 8 --samples 157351936 \
-    --note "build $build; 32-spp profile scaled to the 256-spp frame" --source "$(src_of bdpt)" > /dev/null
-python3 scripts/pmc_traffic.py standard/bdpt tpt_bdpt_ "$p/bdpt_fetch/run_counter_collection.csv" \
-    "$p/bdpt_write/run_counter_collection.csv" --frames 0.125 --note "build $build, 32-spp profile x 8 (profiles/${tag}_bdpt_pmc.txt)" > /dev/null
+if [ -d "$p/pt_kt" ]; then
+  python3 scripts/valu_model.py "$p" standard/pt pt tpt_pt_kernel --frames 2 --samples 629407744 \
+      --note "build $build" --source "$(src_of pt)" > /dev/null
+  python3 scripts/pmc_traffic.py standard/pt tpt_pt_kernel "$p/pt_fetch/run_counter_collection.csv" \
+      "$p/pt_write/run_counter_collection.csv" --frames 2 --note "build $build (profiles/${tag}_pt_pmc.txt)" > /dev/null
+fi
+if [ -d "$p/bdpt_kt" ]; then
+  python3 scripts/valu_model.py "$p" standard/bdpt bdpt tpt_bdpt_ --scale 8 --samples 157351936 \
+      --note "build $build; 32-spp profile scaled to the 256-spp frame" --source "$(src_of bdpt)" > /dev/null
+  python3 scripts/pmc_traffic.py standard/bdpt tpt_bdpt_ "$p/bdpt_fetch/run_counter_collection.csv" \
+      "$p/bdpt_write/run_counter_collection.csv" --frames 0.125 --note "build $build, 32-spp profile x 8 (profiles/${tag}_bdpt_pmc.txt)" > /dev/null
+fi
 if [ -d "$p/c5_kt" ]; then
   python3 scripts/valu_model.py "$p" bunny/bdpt c5 tpt_bdpt_ --scale 128 --samples 2517630976 \
       --note "build $build; 32-spp profile scaled to the 4096-spp frame" --source "$(src_of c5)" > /dev/null
