@@ -2,11 +2,16 @@
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--mode pt|bdpt|c5|pti] [--scene S] [--spp SPP]
 
-With no --mode the ONE JSON line carries three workloads, each a full 784x784 frame
-per step with the flattened scene already resident in HBM:
+With no --mode the ONE JSON line carries every BASELINE config, each a full 784x784
+frame per step with the flattened scene already resident in HBM:
   * the headline, BASELINE.json configs[1]: Standard Cornell Box, PT, 1024 spp;
   * "bdpt": configs[2], Standard Cornell Box, BDPT, 256 spp;
-  * "c5":   configs[4], Cornell + bunny, BDPT, 4096 spp (one frame: ~19 s on one GPU).
+  * "c4_ball" / "c4_smooth": configs[3], refractive ball / smooth dielectric, PT, 4096 spp;
+  * "c5":   configs[4], Cornell + bunny, BDPT, 4096 spp (one frame: ~18 s on one GPU);
+  * configs[0] (PT 16 spp, -j 1, CPU only) is the headline cpu_baseline's "j1" leg;
+  * "shard_model" (N = 1 only): the 1/2/4/8-way pixel split of configs 2, 3 and 5 timed
+    shard by shard on this one GPU (sharding.shard_model): the frame each rank of an
+    N-GPU run would render, its kernel time, and T_full / (N * T_slowest_shard).
 --mode runs one workload alone (profiling runs use it).
 
 With N > 1 (launched by torch.distributed.run, one process per GPU) each rank
@@ -53,13 +58,22 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
 N_SIMD = 1024          # 256 CUs x 4 SIMDs
 MAX_CLOCK_MHZ = 2400.0
 
-# (scene, mode, spp) of each workload; BASELINE.json configs[1], [2], [4]
-WORKLOADS = {"pt": ("standard", "pt", 1024), "bdpt": ("standard", "bdpt", 256), "c5": ("bunny", "bdpt", 4096),
-             "pti": ("standard", "pti", 1024)}
+# (scene, mode, spp) of each workload; BASELINE.json configs[1], [2], [3] (two scenes), [4]
+WORKLOADS = {"pt": ("standard", "pt", 1024), "bdpt": ("standard", "bdpt", 256),
+             "c4_ball": ("refractive_ball", "pt", 4096), "c4_smooth": ("smooth_dielectric", "pt", 4096),
+             "c5": ("bunny", "bdpt", 4096), "pti": ("standard", "pti", 1024)}
 CONFIG_NAME = {"pt": "configs[1]: Standard Cornell Box 784x784, PT, 1024 spp",
                "bdpt": "configs[2]: Standard Cornell Box 784x784, BDPT, 256 spp",
+               "c4_ball": "configs[3]: Refractive Ball Cornell 784x784, PT, 4096 spp",
+               "c4_smooth": "configs[3]: Smooth Dielectric Cornell 784x784, PT, 4096 spp",
                "c5": "configs[4]: Cornell + bunny OBJ 784x784, BDPT, 4096 spp, pixel-sharded + RCCL reduce",
                "pti": "PathTrace with the indirect bounce (not a BASELINE config), Standard 784x784, 1024 spp"}
+# (steps, warmup) of the workloads after the first one in a default run
+SUB_STEPS = {"bdpt": (2, 1), "c4_ball": (2, 1), "c4_smooth": (2, 1), "c5": (1, 0)}
+# shard model: (workload, spp) -- c5 at a reduced spp (its per-iteration launch chain is
+# the same at every spp, so the split's efficiency is too; stated in the line)
+SHARD_MODEL = (("pt", 1024), ("bdpt", 256), ("c5", 256))
+SHARD_NS = (2, 4, 8)
 
 
 def parse():
@@ -67,12 +81,14 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5, help="timed frames of the headline PT workload")
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--mode", choices=("pt", "bdpt", "c5", "pti"), default=None,
-                    help="run one workload alone (default: PT headline + bdpt + c5 in one line)")
+    ap.add_argument("--mode", choices=tuple(WORKLOADS), default=None,
+                    help="run one workload alone (default: PT headline + every other config in one line)")
     ap.add_argument("--scene", default=None, help="override the workload's scene")
     ap.add_argument("--spp", type=int, default=None, help="override the workload's spp")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline legs")
     ap.add_argument("--no-c5", action="store_true", help="default line without the c5 sub-object")
+    ap.add_argument("--no-shard-model", action="store_true", help="default line without the shard_model sub-object")
+    ap.add_argument("--shard-only", action="store_true", help="print the shard_model object alone (A/B runs)")
     ap.add_argument("--sample-seed", action="store_true",
                     help="--mode pt|pti only: per-sample seeding (TPT_FLAG_SAMPLE_SEED), a non-replay throughput mode")
     ap.add_argument("--cpu-threads", type=int, default=None)
@@ -144,6 +160,8 @@ def cpu_baseline(key, scene, mode, threads, info):
     """Bounded CPU sample of the workload on this host: full frames at a reduced spp
     (throughput does not depend on spp: the per-pixel stream is serial either way)."""
     spp = {"pt": 64, "pti": 16, "bdpt": 2}[mode] if key != "c5" else 1
+    if key.startswith("c4"):
+        spp = 32  # the glass / smooth scenes: ~1 s at 16 threads, lengthened below
     dt, kind = cpu_render(scene, mode, spp, threads)
     if dt < 2.0 and mode == "pt":  # many-core host: lengthen the sample to a few seconds
         spp *= max(2, int(round(4.0 / max(dt, 1e-3))))
@@ -156,11 +174,11 @@ def cpu_baseline(key, scene, mode, threads, info):
                      "wall %.2f s" % (mode.upper(), scene, spp, threads, dt),
            "host": info}
     if key == "pt":
-        # BASELINE.json configs[0]: Standard PT 16 spp with -j 1, sampled at 4 spp
-        dt1, kind1 = cpu_render(scene, mode, 4, 1)
-        out["j1"] = {"value": round(784 * 784 * 4 / dt1 / 1e6, 4), "unit": "Msamples/s", "cores": 1,
-                     "kind": kind1, "sample": "configs[0] (-j 1) at 4 spp instead of 16: full 784x784 PT frame "
-                                              "of 'standard', Renderer::Render with 1 thread, wall %.2f s" % dt1}
+        # BASELINE.json configs[0]: Standard PT 16 spp with -j 1, the whole config
+        dt1, kind1 = cpu_render(scene, mode, 16, 1)
+        out["j1"] = {"value": round(784 * 784 * 16 / dt1 / 1e6, 4), "unit": "Msamples/s", "cores": 1,
+                     "kind": kind1, "sample": "configs[0] itself: full 784x784 PT frame of 'standard' at 16 spp, "
+                                              "Renderer::Render with 1 thread (-j 1), wall %.2f s" % dt1}
     return out
 
 
@@ -285,7 +303,8 @@ class Runner:
         samples = W * H * spp * steps  # all ranks together cover the frame each step
         kernel_ms = sum(kms) / len(kms)
         shard_samples = st.samples
-        tkey = "%s/%s" % (scene, mode)
+        # the VALU model is profiled on the replay kernels; a seeded run has no entry
+        tkey = "%s/%s%s" % (scene, mode, "/seeded" if flags else "")
         line = {"metric": "Msamples/s (pixels x spp / s), %s %s %dx%d%s" % (
                     scene, mode.upper(), W, H, ", per-sample seeding (not the reference's replay)" if flags else ""),
                 "value": round(samples / dt / 1e6, 2), "unit": "Msamples/s", "n_gpus": self.world, "steps": steps,
@@ -297,9 +316,39 @@ class Runner:
                            else "1 GPU"},
                 "roofline": valu_roofline(tkey, kernel_ms, shard_samples),
                 "roofline_hbm_model": hbm_model(scene, mode, kernel_ms, shard_samples, tkey),
-                "kernel_ms_per_step": round(kernel_ms, 3), "samples_per_rank_step": shard_samples}
+                "kernel_ms_per_step": round(kernel_ms, 3), "samples_per_rank_step": shard_samples,
+                "nonfinite_pixels": st.nonfinite + st.nonfinite_splat}
         return line
 
+    def shard_model(self):
+        """The N-way pixel split of configs 2, 3 and 5 modelled on this one GPU: every
+        stride-N shard is rendered alone (tpt_render_device, as rank r of an N-GPU run
+        renders it) and timed with the library's HIP events (sharding.shard_model)."""
+        pytpt = self.pytpt
+        out = {"note": "one-GPU model of the N-GPU split, not a scaling run: each stride-N shard "
+                       "(pixels i = r mod N, Renderer.cpp:38) rendered alone on this GPU; eff = T_full / "
+                       "(N x slowest shard), kernel time (HIP events); the reduce (one 7.4 / 14.7 MB RCCL "
+                       "reduce) is not modelled", "ns": list(SHARD_NS)}
+        for key, spp in SHARD_MODEL:
+            scene, mode, _ = WORKLOADS[key]
+            if self.scene != scene:
+                self.ctx.upload(pytpt.Preset(scene))
+                self.scene = scene
+            m = {"pt": pytpt.MODE_PT, "bdpt": pytpt.MODE_BDPT}[mode]
+            fb = self.fb
+
+            def render(begin, stride):
+                st = self.ctx.render_device(spp, m, fb[0].data_ptr(), fb[1].data_ptr(), begin, stride, 0)
+                return st.kernel_ms, st.total_ms
+
+            render(0, 1)  # warm-up
+            res = self.sharding.shard_model(render, SHARD_NS)
+            res["workload"] = "%s %s %d spp%s" % (scene, mode.upper(), spp,
+                                                  "" if spp == WORKLOADS[key][2] else
+                                                  " (configs[4] at a reduced spp: same per-iteration chain)")
+            out[key] = res
+        return out
+    
     def close(self):
         self.ctx.close()
         if self.dist is not None:
@@ -309,6 +358,11 @@ class Runner:
 def main():
     a = parse()
     r = Runner(a)
+    if a.shard_only:
+        r.fb = r.torch.zeros(2, 784 * 784 * 3, dtype=r.torch.float32, device="cuda")
+        print(json.dumps({"shard_model": r.shard_model()}), flush=True)
+        r.close()
+        return
     info = cpu_info()
     want_cpu = not a.no_cpu and r.world == 1 and r.rank == 0
     # every CPU this process may use: the affinity mask, capped by the cgroup's CPU
@@ -316,16 +370,12 @@ def main():
     # than that only time-slice)
     threads = a.cpu_threads or (min(info["affinity"], max(1, int(info["cgroup_cpus"])))
                                 if info["cgroup_cpus"] else info["affinity"])
-    keys = [a.mode] if a.mode else ["pt", "bdpt"] + ([] if a.no_c5 else ["c5"])
+    keys = [a.mode] if a.mode else ["pt", "bdpt", "c4_ball", "c4_smooth"] + ([] if a.no_c5 else ["c5"])
     lines = {}
     for k in keys:
-        if k == keys[0]:
-            steps, warmup = a.steps, a.warmup
-        elif k == "bdpt":
-            steps, warmup = 2, 1      # ~0.63 s per frame on one MI355X
-        else:
-            steps, warmup = 1, 0      # c5: ~19 s per frame on one MI355X
+        steps, warmup = (a.steps, a.warmup) if k == keys[0] else SUB_STEPS[k]
         lines[k] = r.run(k, steps, warmup)
+    shard_model = r.shard_model() if (a.mode is None and r.world == 1 and not a.no_shard_model) else None
     if r.rank == 0:
         if want_cpu:
             for k in keys:
@@ -335,12 +385,16 @@ def main():
         out = {"metric": head["metric"], "value": head["value"], "unit": "Msamples/s", "n_gpus": r.world,
                "steps": head["steps"], "warmup": head["warmup"], "ms_per_step": head["ms_per_step"],
                "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32+f64",
-               "data": "synthetic (deterministic Cornell scenes, reference seeds pixel+1)",
+               "data": "synthetic (deterministic Cornell scenes, %s)" % (
+                   "per-sample seeding: sample j of pixel i seeds tpt_sample_seed(i, j)" if a.sample_seed
+                   else "reference seeds pixel+1"),
                "config": head["config"], "roofline": head["roofline"],
                "roofline_hbm_model": head["roofline_hbm_model"], "cpu_baseline": head.get("cpu_baseline"),
-               "kernel_ms_per_step": head["kernel_ms_per_step"]}
+               "kernel_ms_per_step": head["kernel_ms_per_step"], "nonfinite_pixels": head["nonfinite_pixels"]}
         for k in keys[1:]:
             out[k] = lines[k]
+        if shard_model is not None:
+            out["shard_model"] = shard_model
         print(json.dumps(out), flush=True)
     r.close()
 

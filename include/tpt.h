@@ -36,7 +36,8 @@
 extern "C" {
 #endif
 
-#define TPT_ABI_VERSION 1
+/* 2: tpt_stats gained nonfinite / nonfinite_splat (round 3) */
+#define TPT_ABI_VERSION 2
 
 /* error codes */
 #define TPT_OK 0
@@ -134,6 +135,13 @@ typedef struct tpt_stats {
     int64_t bounces;              /* sum of outBounces (Renderer.cpp:52, 64-bit) */
     double kernel_ms;             /* device time of the integration kernel(s) */
     double total_ms;              /* wall time of tpt_render incl. copies */
+    /* Pixels of this call's output whose radiance (rgb) / splat has a non-finite
+     * component.  The reference's only NaN guard is an MSVC _DEBUG trap
+     * (Vector.hpp:19-22): in a release build a NaN sample poisons its pixel silently
+     * (config 5's frame has one, pixel 485594).  Counted on the device after the
+     * render, outside kernel_ms. */
+    int64_t nonfinite;
+    int64_t nonfinite_splat;
 } tpt_stats;
 
 typedef struct tpt_ctx tpt_ctx;

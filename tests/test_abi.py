@@ -34,7 +34,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version_and_camera():
     L = pytpt.lib()
-    assert L.tpt_abi_version() == 1
+    assert L.tpt_abi_version() == 2
     o = Oracle("standard")
     # CalculateScale(fov) (SceneRenderingHelper.cpp:12-14), host-side, bit-exact
     for fov in (40.0, 60.0, 90.0, 17.5):

@@ -76,6 +76,17 @@ def test_full_image_pt():
     assert eq_bits(img[y:y + 64, x:x + 64], g["pt16_crop"])
 
 
+def test_full_frame_pins_c1():
+    """The whole configs[0] frame (Standard PT 16 spp, 784x784) of the CPU restatement
+    against the real Renderer::Render's, pinned by tests/golden/frame_c1.npz
+    (make_frames.py): sha256 of every float, so the full-frame pins the GPU tests use
+    are themselves checked here."""
+    from frames import check_exact
+    g = golden("frame_c1.npz")
+    img, _ = Oracle("standard").render(0, 16, threads=8)
+    check_exact(img, g, "rgb", "oracle PT16 frame")
+
+
 def test_full_image_bdpt():
     # Renderer::Render with -j1: splat buffers merged after the radiance (Renderer.cpp:98-114)
     g = golden("image_standard.npz")

@@ -282,24 +282,27 @@ TPT_D void camera_vertices(const DScene& s, int64_t i, BVert& c0, BVert& c1) {
 }
 
 // ------------------------------------------------------------ wavefront --
-// Per sample iteration, for every pixel of the shard:
-//   gen:     generate both subpaths (RNG-sequential per pixel) and write them to
-//            HBM as SoA records [path*16+vertex][field][pixel];
-//   scan:    inclusive prefix sums of the strategy counts (s = 0 ones and the others);
-//   scatter: task[g] = (pixel, t, s) for every strategy, the s = 0 (emission-only)
-//            strategies first and the connecting ones after, so a wave holds one
-//            kind (4 B per task; the result slot is the task's own index);
+// A wavefront holds `nb` consecutive sample iterations of n pixel streams: its items
+// are (iteration b, pixel k), item = b * n + k.  For every item:
+//   gen:     generate both subpaths and write them to HBM as vertex records; one lane
+//            runs its pixel's nb samples back to back (the RNG stream is sequential
+//            per pixel), so a small shard still fills a wavefront as large as a full
+//            frame's and the per-wavefront tail is paid once per nb iterations;
+//   scan:    inclusive prefix sums of the strategy counts per item;
+//   scatter: task[g] = (item, t, s) for every strategy, in four class runs, so a
+//            wave holds one kind (4 B per task; the result slot is the task's index);
 //   connect: ONE LANE PER STRATEGY (PathWeight), so a wave's work is 64 strategies
 //            instead of the longest lane's cn*(ln+1) (measured 18 mean vs 73 max);
 //            t = 1 splats go straight to the splat buffer;
-//   fold:    per pixel, result += w over its strategies in (t, s) order (t > 1) and
-//            fb += (1/spp) * result -- the reference's summation order.
+//   fold:    per pixel, for b = 0 .. nb-1 in order: result += w over the item's
+//            strategies in (t, s) order (t > 1), fb += (1/spp) * result -- the
+//            reference's summation order.
 // One vertex record = 64 B = four float4: (x, type|prim) (N, pdf) (alpha, mat) (q1, q8, -, -),
-// laid out [pixel][slot] so a vertex is one contiguous line segment (4 x 16-B accesses).
+// laid out [item][slot] so a vertex is one contiguous line segment (4 x 16-B accesses).
 constexpr int kRecV = 4;  // float4 per vertex record
 struct WfState {
-    float4* rec;          // n * 32 * kRecV float4
-    int* cnt;             // cn | ln << 16
+    float4* rec;          // items * 32 * kRecV float4
+    int* cnt;             // per item: cn | ln << 16
     // strategies per pixel in four classes (task runs, see tpt_bdpt_scatter_kernel):
     //   np  = (s = 0: cn - 1) | (t > 1, s > 1: (cn - 1)(ln - 1)) << 32
     //   np2 = (t > 1, s = 1: cn - 1) | (t = 1: ln) << 32
@@ -307,16 +310,24 @@ struct WfState {
     unsigned long long* incl;   // inclusive scan of np (both halves at once)
     unsigned long long* np2;
     unsigned long long* incl2;  // inclusive scan of np2
-    unsigned* task;       // strategy -> pixel | t << 22 | s << 27 (pixel < kWfChunk)
+    unsigned* task;       // strategy -> item | t << 22 | s << 27 (item < kWfChunk)
     float* res;           // 3 floats per strategy, in task order
-    uint32_t* rng;        // XorShift state per pixel stream
+    // Per pixel stream: (wavefronts completed) << 32 | XorShift32 state.  Consecutive
+    // wavefronts' gen kernels run concurrently (two streams): the lane that finishes
+    // pixel k's samples of wavefront f publishes seq f + 1 with the state in ONE 64-bit
+    // agent-scope atomic store, and gen(f + 1) starts pixel k once it reads seq f + 1.
+    unsigned long long* rngseq;
+    int* stall;           // set when a gen lane gave up waiting (watchdog); never in a good run
     float* acc;           // 3 floats per pixel
     const int64_t* list;  // pixel list (or null: begin + k*stride)
-    int64_t begin, stride, n;
+    int64_t begin, stride, n;  // n: pixel streams
+    int nb;                    // sample iterations in this wavefront (items = nb * n)
+    int64_t ni;                // items = nb * n
     unsigned long long* bounces;
 };
-// One wavefront holds at most kWfChunk pixel streams (launch() splits larger shards):
-// the task record keeps the pixel in 22 bits and the per-class scans count in 32.
+// One wavefront holds at most kWfChunk items (launch() splits larger shards, and sizes
+// nb so that nb * n <= kWfChunk): the task record keeps the item in 22 bits and the
+// per-class scans count in 32.
 constexpr int64_t kWfChunk = int64_t(1) << 22;
 constexpr unsigned kTaskPixelMask = (unsigned)kWfChunk - 1;
 static_assert(kMaxLen < 32, "task records keep t and s in 5 bits each");

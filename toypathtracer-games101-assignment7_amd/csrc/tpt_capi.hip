@@ -367,29 +367,83 @@ __global__ __launch_bounds__(kBlock, TPT_PTI_MINWAVES) void tpt_pti_kernel(DScen
 #define TPT_CONN_MINWAVES 4  // waves per SIMD (measured: 4 beats 2, 3 and 5)
 #endif
 
-// Path generation, persistent: each lane runs a pixel's sample as a sequence of
-// steps (start, camera-path vertex..., light start, light-path vertex...) and takes
-// the next pixel from its shard's queue as soon as it is done, so a wave stays full
-// although path lengths differ per lane (a lane-per-pixel grid ran at 44 % lane
-// efficiency).  Per-pixel order -- and so every RNG draw -- is unchanged.  Queues:
-// one counter per shard of pixels, shard = blockIdx.x % 8 (blocks b and b + 8 are
-// dealt to the same XCD; speed only).
+// Path generation, persistent: each lane runs a pixel's nb samples (the wavefront's
+// iterations) as a sequence of steps (start, camera-path vertex..., light start,
+// light-path vertex..., then the next sample of the same pixel) and takes the next
+// pixel from its shard's queue as soon as it is done, so a wave stays full although
+// path lengths differ per lane (a lane-per-pixel grid ran at 44 % lane efficiency).
+// Per-pixel order -- and so every RNG draw -- is unchanged.  Queues: one counter per
+// shard of pixels, shard = blockIdx.x % 8 (blocks b and b + 8 are dealt to the same
+// XCD; speed only).  `batch`: this wavefront's ordinal in the chunk (0: the streams
+// start at ResetRandom(i + 1); >= 2: this buffer already holds the camera vertices).
+//
+// Wavefront f's gen runs beside wavefront f - 1's (another stream): a lane that claims
+// pixel k waits, inside the persistent loop, until gen(f - 1) has published k's stream
+// state (WfState::rngseq), so gen(f)'s tail of long paths no longer idles the chip
+// until gen(f + 1) may start.  gen(f - 1) never waits on gen(f), so it always drains.
+// A watchdog (kStallTicks of the 100 MHz real-time counter) ends a wait that cannot
+// finish -- never expected -- by flagging w.stall and giving the pixel no strategies,
+// so a broken pipeline is reported as an error instead of hanging the GPU.
+#ifndef TPT_WATCHDOG
+#define TPT_WATCHDOG 1
+#endif
+#ifndef TPT_STALL_TICKS
+#define TPT_STALL_TICKS 2000000000u  // 20 s at 100 MHz (32-bit differences wrap at 42 s)
+#endif
+constexpr uint32_t kStallTicks = TPT_STALL_TICKS;
+TPT_D unsigned long long load_rngseq(const unsigned long long* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+TPT_D void store_rngseq(unsigned long long* p, unsigned long long v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 template <int kSc>
-__global__ __launch_bounds__(kBlock, TPT_GEN_MINWAVES) void tpt_bdpt_gen_kernel(DScene s, WfState w, int iter,
+__global__ __launch_bounds__(kBlock, TPT_GEN_MINWAVES) void tpt_bdpt_gen_kernel(DScene s, WfState w, int batch,
                                                                                unsigned* __restrict__ queue) {
     stage_scene<kSc>(s);
     __shared__ QScratch qsm[kBlock / 64];  // compacted flat queries (tpt_device.h)
     s.qs = qsm;
     const int shard = blockIdx.x & 7;
-    const int64_t k_lo = w.n * shard / 8, k_hi = w.n * (shard + 1) / 8;
+    // pixel ordinals and items are < kWfChunk = 2^22: 32-bit indices in the loop
+    const int nn = (int)w.n;
+    const int k_lo = (int)(w.n * shard / 8), k_hi = (int)(w.n * (shard + 1) / 8);
     unsigned* q = queue + shard * 16;  // 64 B apart
-    int64_t k = -1;   // this lane's pixel ordinal (-1: none)
+    int k = -1;       // this lane's pixel ordinal (-1: none)
+    int b = 0;        // its current sample in the wavefront (item b * n + k)
     int phase = 0;    // 0: camera path, 1: light start pending, 2: light path
     int i = 0, cn = 0;
     uint32_t rs = 0;
     unsigned long long nbounce = 0;
     bool drained = false;
     BVert prev, cur;
+    // The camera vertices v0 / v1 of item (b, k): GenerateCameraPath's first two
+    // vertices (BDPT.cpp:41-59) do not depend on the sample (no jitter).  From the
+    // third wavefront of the chunk on, this buffer's slots 0/1 of every item still hold
+    // them (their q1/q8 may be stale; those of vertices cn-2, cn-1 are never read);
+    // before, sample 0 traces them and the later samples copy them from item (0, k).
+    auto start_sample = [&]() {
+        const int it = b * nn + k;
+        BVert c0, c1;
+        if (batch >= 2 || b > 0) {
+            GlobPaths P;
+            P.rec = rec_at(w.rec, batch >= 2 ? it : k, 0);
+            c0 = P.cam(0);
+            c1 = P.cam(1);
+        } else {
+            camera_vertices(s, wf_pixel(w, k), c0, c1);
+        }
+        if (batch < 2) {
+            rec_store(w, 0, it, c0);
+            rec_store(w, 1, it, c1);
+        }
+        prev = c0;
+        cur = c1;
+        i = 1;
+        phase = 0;
+    };
+    bool ready = false;                 // k's stream state is in rs (its previous wavefront is done)
+    bool fresh = false;                 // sample b of k starts at the top of the next step
+    uint32_t wait_t0 = 0;               // when this lane started waiting for k (low 32 bits)
     for (;;) {
         const bool need = k < 0 && !drained;
         const unsigned long long nm = __ballot(need);
@@ -399,40 +453,52 @@ __global__ __launch_bounds__(kBlock, TPT_GEN_MINWAVES) void tpt_bdpt_gen_kernel(
             if (lane_id() == leader) base = atomicAdd(q, (unsigned)__popcll(nm));
             base = __shfl(base, leader);
             if (need) {
-                const int64_t kk = k_lo + base + __popcll(nm & ((1ull << lane_id()) - 1));
+                const int kk = k_lo + (int)base + __popcll(nm & ((1ull << lane_id()) - 1));
                 if (kk < k_hi) {
                     k = kk;
-                    const int64_t pix = wf_pixel(w, k);
-                    BVert c0, c1;
-                    if (iter >= 2) {
-                        // GenerateCameraPath's v0/v1 do not depend on the sample (no
-                        // jitter): this buffer's slots 0/1 still hold them from iteration
-                        // iter - 2 (their q1/q8 may be stale; those of vertices cn-2,
-                        // cn-1 are never read).
-                        GlobPaths P;
-                        P.rec = rec_at(w.rec, k, 0);
-                        c0 = P.cam(0);
-                        c1 = P.cam(1);
-                    } else {
-                        camera_vertices(s, pix, c0, c1);
-                        rec_store(w, 0, k, c0);
-                        rec_store(w, 1, k, c1);
-                    }
-                    rs = iter == 0 ? (uint32_t)((int)pix + 1) : w.rng[k];  // ResetRandom(i + 1), Renderer.cpp:42
-                    if (iter == 0) { w.acc[3 * k] = 0.0f; w.acc[3 * k + 1] = 0.0f; w.acc[3 * k + 2] = 0.0f; }
-                    prev = c0;
-                    cur = c1;
-                    i = 1;
-                    phase = 0;
+                    b = 0;
+                    ready = false;
+                    wait_t0 = (uint32_t)__builtin_amdgcn_s_memrealtime();
                 } else {
                     drained = true;
                 }
             }
         }
+        if (k >= 0 && !ready) {
+            if (batch == 0) {
+                rs = (uint32_t)((int)wf_pixel(w, k) + 1);  // ResetRandom(i + 1), Renderer.cpp:42
+                w.acc[3 * k] = 0.0f; w.acc[3 * k + 1] = 0.0f; w.acc[3 * k + 2] = 0.0f;
+                ready = true;
+            } else {
+                const unsigned long long v = load_rngseq(w.rngseq + k);
+                if ((v >> 32) == (unsigned long long)batch) {
+                    rs = (uint32_t)v;
+                    ready = true;
+                } else if (TPT_WATCHDOG && (uint32_t)__builtin_amdgcn_s_memrealtime() - wait_t0 > kStallTicks) {
+                    // watchdog: give up on k, publish it so later wavefronts do not wait
+                    // too, and report it.  Its items keep older contents, which are
+                    // always a complete sample's (ensure_wf zeroes the arrays when it
+                    // allocates them), so the scan, scatter and connect stay in bounds.
+                    store_rngseq(w.rngseq + k, (unsigned long long)(batch + 1) << 32 | 1u);
+                    atomicOr(w.stall, 1);
+                    k = -1;
+                }
+            }
+            fresh = ready;
+        }
+        if (fresh) {  // one call site: camera_vertices (a closest-hit query) is inlined once
+            start_sample();
+            fresh = false;
+        }
         if (__ballot(k >= 0) == 0) break;  // every lane idle and its shard drained
-        if (k < 0) continue;
+        const bool run = k >= 0 && ready;
+        // The whole wave waits on gen(f - 1): back off.  (No `continue` on this uniform
+        // branch: that form of the loop spilled 120 B/lane instead of 52.)
+        if (__ballot(run) == 0) __builtin_amdgcn_s_sleep(8);
+        if (!run) continue;
+        const int it = b * nn + k;
         int ln = -1;  // >= 0: the pixel's sample is complete
-        if (!gen_step(s, w, k, phase, prev, cur, i, rs)) {
+        if (!gen_step(s, w, it, phase, prev, cur, i, rs)) {
             if (phase == 0) {
                 cn = i + 1;
                 phase = 1;
@@ -441,12 +507,17 @@ __global__ __launch_bounds__(kBlock, TPT_GEN_MINWAVES) void tpt_bdpt_gen_kernel(
             }
         }
         if (ln >= 0) {
-            w.rng[k] = rs;
-            w.cnt[k] = cn | (ln << 16);
-            w.np[k] = (unsigned long long)(cn - 1) | ((unsigned long long)((cn - 1) * (ln - 1)) << 32);
-            w.np2[k] = (unsigned long long)(cn - 1) | ((unsigned long long)ln << 32);
+            w.cnt[it] = cn | (ln << 16);
+            w.np[it] = (unsigned long long)(cn - 1) | ((unsigned long long)((cn - 1) * (ln - 1)) << 32);
+            w.np2[it] = (unsigned long long)(cn - 1) | ((unsigned long long)ln << 32);
             nbounce += (unsigned long long)(cn + ln);
-            k = -1;
+            if (++b < w.nb) {
+                fresh = true;  // the pixel's next sample, same stream, from the next step
+            } else {
+                store_rngseq(w.rngseq + k, (unsigned long long)(batch + 1) << 32 | rs);
+                k = -1;
+                ready = false;
+            }
         }
     }
     atomicAdd(w.bounces, nbounce);
@@ -464,9 +535,9 @@ struct StratRange {
     int64_t b[4];        // the pixel's start in each run (absolute task index)
     int ln, np;          // light vertices, strategies
 };
-TPT_D StratRange strat_range(const WfState& w, int64_t k) {
+TPT_D StratRange strat_range(const WfState& w, int64_t k) {  // k: item
     const unsigned long long e1 = w.incl[k], c1 = w.np[k], e2 = w.incl2[k], c2 = w.np2[k];
-    const unsigned long long t1 = w.incl[w.n - 1], t2 = w.incl2[w.n - 1];
+    const unsigned long long t1 = w.incl[w.ni - 1], t2 = w.incl2[w.ni - 1];
     const int64_t totA = (int64_t)(t1 & 0xffffffffull), totE = (int64_t)(t1 >> 32), totD = (int64_t)(t2 & 0xffffffffull);
     const int64_t xA = (int64_t)(e1 & 0xffffffffull) - (int64_t)(c1 & 0xffffffffull);
     const int64_t xE = (int64_t)(e1 >> 32) - (int64_t)(c1 >> 32);
@@ -482,14 +553,14 @@ TPT_D StratRange strat_range(const WfState& w, int64_t k) {
     return r;
 }
 TPT_D int64_t total_tasks(const WfState& w) {
-    const unsigned long long t1 = w.incl[w.n - 1], t2 = w.incl2[w.n - 1];
+    const unsigned long long t1 = w.incl[w.ni - 1], t2 = w.incl2[w.ni - 1];
     return (int64_t)(t1 & 0xffffffffull) + (int64_t)(t1 >> 32) + (int64_t)(t2 & 0xffffffffull) + (int64_t)(t2 >> 32);
 }
 
 __global__ __launch_bounds__(kBlock) void tpt_bdpt_scatter_kernel(WfState w, unsigned* __restrict__ queue) {
-    const int64_t k = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (k < 8) queue[k * 16] = 0;  // gen of the next iteration (same stream, after this kernel) starts its shards at 0
-    if (k >= w.n) return;
+    const int64_t k = (int64_t)blockIdx.x * kBlock + threadIdx.x;  // item
+    if (k < 8) queue[k * 16] = 0;  // gen of the next wavefront (same stream, after this kernel) starts its shards at 0
+    if (k >= w.ni) return;
     const StratRange r = strat_range(w, k);
     const int ln = r.ln, cn = w.cnt[k] & 0xffff;
     const unsigned kk = (unsigned)k;
@@ -543,22 +614,25 @@ __global__ __launch_bounds__(kBlock, TPT_CONN_MINWAVES) void tpt_bdpt_conn_kerne
 #define TPT_FLAT_DEFAULT 3  // kFlatShadow | kFlatHit; measured: BDPT 882 -> 812 ms, PT 64.0 -> 61.3 ms
 #endif
 __global__ __launch_bounds__(kBlock) void tpt_bdpt_fold_kernel(WfState w, float inv) {
-    const int64_t k = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const int64_t k = (int64_t)blockIdx.x * kBlock + threadIdx.x;  // pixel
     if (k >= w.n) return;
-    const StratRange r = strat_range(w, k);
-    const int ln = r.ln, cn = w.cnt[k] & 0xffff;
-    V3 res = v3s(0.0f);  // BDPT.cpp:289 `Vector3f result;`
-    // the t > 1 strategies in (t, s) order (t = 1 ones were splatted), each read from
-    // its place in the task runs -- the same positions tpt_bdpt_scatter_kernel wrote
-    auto add = [&](int64_t g) { res = res + v3(w.res[3 * g], w.res[3 * g + 1], w.res[3 * g + 2]); };
-    for (int t = 2; t <= cn; ++t) {
-        add(r.b[0] + (t - 2));  // s = 0
-        add(r.b[2] + (t - 2));  // s = 1
-        const int64_t g1 = r.b[1] + (int64_t)(t - 2) * (ln - 1) - 2;
-        for (int sl = 2; sl <= ln; ++sl) add(g1 + sl);
-    }
     V3 acc = v3(w.acc[3 * k], w.acc[3 * k + 1], w.acc[3 * k + 2]);
-    acc = acc + mul(res, inv);  // Renderer.cpp:49 `fb[i] += (1.0f / spp) * BDPT(...)`
+    for (int b = 0; b < w.nb; ++b) {  // the pixel's samples in order
+        const int64_t it = (int64_t)b * w.n + k;
+        const StratRange r = strat_range(w, it);
+        const int ln = r.ln, cn = w.cnt[it] & 0xffff;
+        V3 res = v3s(0.0f);  // BDPT.cpp:289 `Vector3f result;`
+        // the t > 1 strategies in (t, s) order (t = 1 ones were splatted), each read from
+        // its place in the task runs -- the same positions tpt_bdpt_scatter_kernel wrote
+        auto add = [&](int64_t g) { res = res + v3(w.res[3 * g], w.res[3 * g + 1], w.res[3 * g + 2]); };
+        for (int t = 2; t <= cn; ++t) {
+            add(r.b[0] + (t - 2));  // s = 0
+            add(r.b[2] + (t - 2));  // s = 1
+            const int64_t g1 = r.b[1] + (int64_t)(t - 2) * (ln - 1) - 2;
+            for (int sl = 2; sl <= ln; ++sl) add(g1 + sl);
+        }
+        acc = acc + mul(res, inv);  // Renderer.cpp:49 `fb[i] += (1.0f / spp) * BDPT(...)`
+    }
     w.acc[3 * k] = acc.x;
     w.acc[3 * k + 1] = acc.y;
     w.acc[3 * k + 2] = acc.z;
@@ -576,6 +650,24 @@ __global__ __launch_bounds__(kBlock) void tpt_bdpt_out_kernel(WfState w, float* 
 __global__ void tpt_scale_kernel(float* __restrict__ buf, int64_t n, float spp) {
     const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k < n) buf[k] = buf[k] * 1.0f / spp;  // Renderer.cpp:59 `e * 1.0f / spp`
+}
+
+// tpt_stats.nonfinite / nonfinite_splat: rows (pixels) of `buf` with a non-finite
+// component, one atomic per wave.  The reference traps NaN only in MSVC _DEBUG builds
+// (Vector.hpp:19-22); a release build carries a NaN sample into its pixel silently.
+__global__ __launch_bounds__(kBlock) void tpt_count_nonfinite_kernel(const float* __restrict__ buf, int64_t rows,
+                                                                     unsigned long long* __restrict__ out) {
+    unsigned long long n = 0;
+    for (int64_t k = (int64_t)blockIdx.x * kBlock + threadIdx.x; k - lane_id() < rows;
+         k += (int64_t)gridDim.x * kBlock) {
+        bool bad = false;
+        if (k < rows) {
+            const float x = buf[3 * k], y = buf[3 * k + 1], z = buf[3 * k + 2];
+            bad = !(__builtin_isfinite(x) && __builtin_isfinite(y) && __builtin_isfinite(z));
+        }
+        n += (unsigned long long)__popcll(__ballot(bad));
+    }
+    if (lane_id() == 0 && n) atomicAdd(out, n);
 }
 
 // Closest-hit queries (Scene::Intersect) for tpt_intersect.
@@ -617,7 +709,7 @@ struct tpt_ctx {
     float* rows = nullptr;
     int64_t rows_cap = 0;
     unsigned long long* counters = nullptr;
-    unsigned* queue = nullptr;  // persistent gen: 8 shard counters, 64 B apart
+    unsigned* queue = nullptr;  // persistent gen: 8 shard counters, 64 B apart, per wavefront buffer
     int num_cu = 0;
     int sc = 0;  // kernel scene class (stage_scene): 0 no LDS, 1 small flat scene, 2 flat + treelets / walk groups
     // wavefront BDPT state (sized for wf_cap pixels)
@@ -625,8 +717,10 @@ struct tpt_ctx {
     int64_t wf_cap = 0;
     WfState wf[2]{};                  // double-buffered: gen(it+1) overlaps connect(it)
     hipStream_t stream2 = nullptr;    // connect + fold
-    hipEvent_t ev_gen[2]{}, ev_fold[2]{};
-    void* scan_tmp = nullptr;
+    hipStream_t stream3 = nullptr;    // gen / scan / scatter of the odd wavefronts (even ones: stream)
+    hipEvent_t ev_gen[2]{}, ev_fold[2]{}, ev_start = nullptr;
+    void* scan_tmp = nullptr;         // two scratch areas: the gen streams scan concurrently
+    void* scan_tmp_g[2]{};
     size_t scan_bytes = 0;
 };
 
@@ -670,8 +764,10 @@ int ensure_fb(tpt_ctx* c) {
     return TPT_OK;
 }
 
-// Wavefront BDPT buffers for n pixel streams: path records (1.7 KB / pixel) and the
-// strategy list (<= 271 strategies / pixel: cn, ln <= 16).
+// Wavefront BDPT buffers for n items (iteration, pixel stream): path records (2 KB per
+// item) and the strategy list (<= 271 strategies per item: cn, ln <= 16).  The per-pixel
+// rng / acc arrays are sized for n pixels too (a wavefront never has more pixels than
+// items).
 int ensure_wf(tpt_ctx* c, int64_t n) {
     if (n <= c->wf_cap) return TPT_OK;
     if (c->wf_mem) (void)hipFree(c->wf_mem);
@@ -683,8 +779,9 @@ int ensure_wf(tpt_ctx* c, int64_t n) {
     const int64_t b_rec = al(2 * kMaxLen * kRecV * n * 16), b_i = al(n * 4), b_l = al(n * 8),
                   b_own = al(n * maxs * 4), b_res = al(n * maxs * 12), b_acc = al(n * 12);
     const int64_t per_buf = b_rec + b_i + 4 * b_l + b_own + b_res;
-    const int64_t total = 2 * per_buf + b_i + b_acc;
+    const int64_t total = 2 * per_buf + b_l + b_acc;
     HIP_TRY(c, hipMalloc(&c->wf_mem, total));
+
     char* p = (char*)c->wf_mem;
     for (int b = 0; b < 2; ++b) {
         WfState& w = c->wf[b];
@@ -697,13 +794,25 @@ int ensure_wf(tpt_ctx* c, int64_t n) {
         w.task = (unsigned*)p; p += b_own;
         w.res = (float*)p; p += b_res;
     }
-    c->wf[0].rng = c->wf[1].rng = (uint32_t*)p; p += b_i;
+    c->wf[0].rngseq = c->wf[1].rngseq = (unsigned long long*)p; p += b_l;
+    // Every item's (cnt, np, np2) starts as a valid empty sample, so a wavefront whose
+    // gen watchdog fired (a lane gave up on its pixel) still scans and scatters in
+    // bounds.  Per array (each < 32 MB per wavefront buffer at a frame's size), on the
+    // context's stream ahead of the first launch.
+    for (int b = 0; b < 2; ++b) {
+        HIP_TRY(c, hipMemsetAsync(c->wf[b].cnt, 0, n * sizeof(int), c->stream));
+        HIP_TRY(c, hipMemsetAsync(c->wf[b].np, 0, n * sizeof(unsigned long long), c->stream));
+        HIP_TRY(c, hipMemsetAsync(c->wf[b].np2, 0, n * sizeof(unsigned long long), c->stream));
+    }
     c->wf[0].acc = c->wf[1].acc = (float*)p;
     const WfState& w = c->wf[0];
     size_t bytes = 0;
     HIP_TRY(c, rocprim::inclusive_scan(nullptr, bytes, w.np, w.incl, (size_t)n, rocprim::plus<unsigned long long>(),
                                        c->stream));
-    HIP_TRY(c, hipMalloc(&c->scan_tmp, bytes));
+    bytes = (bytes + 255) & ~(size_t)255;
+    HIP_TRY(c, hipMalloc(&c->scan_tmp, 2 * bytes));
+    c->scan_tmp_g[0] = c->scan_tmp;
+    c->scan_tmp_g[1] = (char*)c->scan_tmp + bytes;
     c->scan_bytes = bytes;
     c->wf_cap = n;
     return TPT_OK;
@@ -714,30 +823,13 @@ int64_t shard_count(int64_t npix, int64_t begin, int64_t stride) {
     return (npix - begin + stride - 1) / stride;
 }
 
-// One BDPT wavefront over `count` (<= kWfChunk) pixel streams.
-int launch_bdpt_chunk(tpt_ctx* c, int spp, int64_t begin, int64_t stride, int64_t count, const int64_t* dlist,
-                      float* drows, float* dsplat) {
-    const size_t shmem = (size_t)c->ds.lds_bytes;
-    // Two streams: gen/scan/scatter of iteration it on c->stream, connect/fold on
-    // c->stream2, with the wavefront state double-buffered so gen(it+1) runs
-    // beside connect(it) and fills the tail of each.  Ordering per pixel is kept:
-    // gen is sequential on one stream (RNG state), fold is sequential on the other
-    // (acc, splat), and buffer b is rewritten by gen(it+2) only after fold(it).
-    hipStream_t s2 = TPT_BDPT_SERIAL ? c->stream : c->stream2;
-    HIP_TRY(c, hipEventRecord(c->ev_fold[0], c->stream));
-    HIP_TRY(c, hipStreamWaitEvent(s2, c->ev_fold[0], 0));  // stream2 starts after ev0
-    const unsigned pblocks = (unsigned)((count + kBlock - 1) / kBlock);
-#ifndef TPT_CONN_GRID
-#define TPT_CONN_GRID 8192
+#ifndef TPT_WF_ITEMS
+// Items a BDPT wavefront aims for: a shard of n pixel streams runs
+// nb = max(1, TPT_WF_ITEMS / n) sample iterations per wavefront, so a small shard
+// (1/8 of a frame on each of 8 GPUs) launches and drains as few wavefronts as a
+// whole frame does.  Default: one 784 x 784 frame's worth.
+#define TPT_WF_ITEMS 614656
 #endif
-    const unsigned cblocks = (unsigned)std::min<int64_t>(TPT_CONN_GRID, (count * 24 + kBlock - 1) / kBlock + 1);
-    // persistent gen grid: as many workgroups as are resident at once, a multiple of
-    // the 8 queue shards, and no more than the pixels need
-    const auto gen_k = c->sc == 2 ? tpt_bdpt_gen_kernel<2> : c->sc == 1 ? tpt_bdpt_gen_kernel<1> : tpt_bdpt_gen_kernel<0>;
-    const auto conn_k = c->sc == 2 ? tpt_bdpt_conn_kernel<2> : c->sc == 1 ? tpt_bdpt_conn_kernel<1> : tpt_bdpt_conn_kernel<0>;
-    int per_cu = 0;
-    HIP_TRY(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                   &per_cu, (const void*)gen_k, kBlock, shmem));
 #ifndef TPT_GEN_GRID_Q
 // gen's persistent grid, in 32nds of what fits on the chip at once.  A full grid
 // occupies every CU until the queue drains, so connect (other stream) only runs in
@@ -746,36 +838,93 @@ int launch_bdpt_chunk(tpt_ctx* c, int spp, int64_t begin, int64_t stride, int64_
 // 1173, 10 -> 553 / 1131, 11 -> 556 / 1108, 12 -> 567 / -, 16 -> 585 / -.
 #define TPT_GEN_GRID_Q 11
 #endif
-    int64_t gb = (int64_t)std::max(per_cu, 1) * std::max(c->num_cu, 1) * TPT_GEN_GRID_Q / 32;
+#ifndef TPT_GEN2_MIN_NB
+#define TPT_GEN2_MIN_NB 2  // two gen streams when a wavefront holds >= this many iterations
+#endif
+int wf_iters(int64_t count, int spp) {
+    const int64_t nb = std::max<int64_t>(1, std::min<int64_t>((int64_t)TPT_WF_ITEMS, kWfChunk) / std::max<int64_t>(count, 1));
+    // at least four wavefronts where spp allows, so gen(f + 1) has connect(f) to overlap
+    return (int)std::min<int64_t>(nb, std::max(1, spp / 4));
+}
+
+// The BDPT sample loop over `count` (<= kWfChunk) pixel streams, as wavefronts of
+// nb = wf_iters(count, spp) sample iterations each.
+int launch_bdpt_chunk(tpt_ctx* c, int spp, int64_t begin, int64_t stride, int64_t count, const int64_t* dlist,
+                      float* drows, float* dsplat) {
+    const size_t shmem = (size_t)c->ds.lds_bytes;
+    // Two streams: gen/scan/scatter of wavefront f on c->stream, connect/fold on
+    // c->stream2, with the wavefront state double-buffered so gen(f+1) runs beside
+    // connect(f) and fills the tail of each.  Ordering per pixel is kept: gen is
+    // sequential on one stream (RNG state), fold is sequential on the other (acc,
+    // splat), and buffer b is rewritten by gen(f+2) only after fold(f).
+    // Streams: gen / scan / scatter of wavefront f on gs[f & 1] (the two gen streams let
+    // gen(f + 1) start while gen(f) drains its long paths; they hand each pixel's
+    // stream state over through WfState::rngseq), connect / fold of every wavefront on
+    // s2.  The wavefront state is double-buffered: buffer f & 1 is rewritten by
+    // gen(f + 2) only after fold(f).  Per pixel the order is kept: gen(f) samples after
+    // gen(f - 1) (rngseq), fold is sequential on s2 (acc, splat).
+    const int nb = wf_iters(count, spp);
+    hipStream_t s2 = TPT_BDPT_SERIAL ? c->stream : c->stream2;
+    // The second gen stream only where wavefronts hold several iterations (small
+    // shards: a lane runs nb samples of one pixel, so gen's tail is long).  For a
+    // frame-sized shard (nb = 1) gen(f + 1)'s lanes would mostly sit waiting on
+    // gen(f)'s pixels and take slots from connect: same-box 452 vs 477 ms (Standard
+    // BDPT 256 spp); at 1/8 of the frame the two streams win, 0.72 -> 0.81 of linear.
+    const bool two_gen = !TPT_BDPT_SERIAL && nb >= TPT_GEN2_MIN_NB;
+    hipStream_t gs[2] = {c->stream, two_gen ? c->stream3 : c->stream};
+    // both gen streams start after everything queued so far; the pixel states and the
+    // queue counters of both buffers start at 0
+    HIP_TRY(c, hipMemsetAsync(c->wf[0].rngseq, 0, count * sizeof(unsigned long long), c->stream));
+    HIP_TRY(c, hipMemsetAsync(c->queue, 0, 2 * 8 * 64, c->stream));
+    HIP_TRY(c, hipEventRecord(c->ev_start, c->stream));
+    HIP_TRY(c, hipStreamWaitEvent(s2, c->ev_start, 0));
+    if (gs[1] != gs[0]) HIP_TRY(c, hipStreamWaitEvent(gs[1], c->ev_start, 0));
+    const unsigned pblocks = (unsigned)((count + kBlock - 1) / kBlock);
+#ifndef TPT_CONN_GRID
+#define TPT_CONN_GRID 8192
+#endif
+    const int gen_q = TPT_GEN_GRID_Q;
+    // persistent gen grid: as many workgroups as are resident at once, a multiple of
+    // the 8 queue shards, and no more than the pixels need
+    const auto gen_k = c->sc == 2 ? tpt_bdpt_gen_kernel<2> : c->sc == 1 ? tpt_bdpt_gen_kernel<1> : tpt_bdpt_gen_kernel<0>;
+    const auto conn_k = c->sc == 2 ? tpt_bdpt_conn_kernel<2> : c->sc == 1 ? tpt_bdpt_conn_kernel<1> : tpt_bdpt_conn_kernel<0>;
+    int per_cu = 0;
+    HIP_TRY(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                   &per_cu, (const void*)gen_k, kBlock, shmem));
+    int64_t gb = (int64_t)std::max(per_cu, 1) * std::max(c->num_cu, 1) * gen_q / 32;
     gb = std::min<int64_t>(gb, ((int64_t)pblocks + 7) / 8 * 8);
     const unsigned gblocks = (unsigned)std::max<int64_t>(8, gb / 8 * 8);
     const float inv = 1.0f / spp;
-    for (int it = 0; it < spp; ++it) {
-        const int b = it & 1;
+    for (int f = 0, it0 = 0; it0 < spp; ++f, it0 += nb) {
+        const int b = f & 1;
         WfState w = c->wf[b];
         w.list = dlist;
         w.begin = begin;
         w.stride = stride;
         w.n = count;
+        w.nb = std::min(nb, spp - it0);
+        w.ni = (int64_t)w.nb * count;
         w.bounces = c->counters;
-        if (it >= 2) HIP_TRY(c, hipStreamWaitEvent(c->stream, c->ev_fold[b], 0));
-        if (it == 0) HIP_TRY(c, hipMemsetAsync(c->queue, 0, 8 * 64, c->stream));  // later: reset by scatter
-        hipLaunchKernelGGL(gen_k, dim3(gblocks), dim3(kBlock), shmem, c->stream, c->ds, w, it, c->queue);
+        w.stall = reinterpret_cast<int*>(c->counters + 4);
+        unsigned* queue = c->queue + b * 8 * 16;
+        const unsigned iblocks = (unsigned)((w.ni + kBlock - 1) / kBlock);
+        const unsigned cblocks = (unsigned)std::min<int64_t>(TPT_CONN_GRID, (w.ni * 24 + kBlock - 1) / kBlock + 1);
+        if (f >= 2) HIP_TRY(c, hipStreamWaitEvent(gs[b], c->ev_fold[b], 0));
+        hipLaunchKernelGGL(gen_k, dim3(gblocks), dim3(kBlock), shmem, gs[b], c->ds, w, f, queue);
         size_t bytes = c->scan_bytes;
-        HIP_TRY(c, rocprim::inclusive_scan(c->scan_tmp, bytes, w.np, w.incl, (size_t)count,
-                                           rocprim::plus<unsigned long long>(),
-                                           c->stream));
+        HIP_TRY(c, rocprim::inclusive_scan(c->scan_tmp_g[b], bytes, w.np, w.incl, (size_t)w.ni,
+                                           rocprim::plus<unsigned long long>(), gs[b]));
         bytes = c->scan_bytes;
-        HIP_TRY(c, rocprim::inclusive_scan(c->scan_tmp, bytes, w.np2, w.incl2, (size_t)count,
-                                           rocprim::plus<unsigned long long>(), c->stream));
-        hipLaunchKernelGGL(tpt_bdpt_scatter_kernel, dim3(pblocks), dim3(kBlock), 0, c->stream, w, c->queue);
-        HIP_TRY(c, hipEventRecord(c->ev_gen[b], c->stream));
+        HIP_TRY(c, rocprim::inclusive_scan(c->scan_tmp_g[b], bytes, w.np2, w.incl2, (size_t)w.ni,
+                                           rocprim::plus<unsigned long long>(), gs[b]));
+        hipLaunchKernelGGL(tpt_bdpt_scatter_kernel, dim3(iblocks), dim3(kBlock), 0, gs[b], w, queue);
+        HIP_TRY(c, hipEventRecord(c->ev_gen[b], gs[b]));
         HIP_TRY(c, hipStreamWaitEvent(s2, c->ev_gen[b], 0));
         hipLaunchKernelGGL(conn_k, dim3(cblocks), dim3(kBlock), shmem, s2, c->ds, w, dsplat);
         hipLaunchKernelGGL(tpt_bdpt_fold_kernel, dim3(pblocks), dim3(kBlock), 0, s2, w, inv);
         HIP_TRY(c, hipEventRecord(c->ev_fold[b], s2));
+        if (it0 + w.nb >= spp) HIP_TRY(c, hipStreamWaitEvent(c->stream, c->ev_fold[b], 0));
     }
-    HIP_TRY(c, hipStreamWaitEvent(c->stream, c->ev_fold[(spp - 1) & 1], 0));
     WfState w = c->wf[0];
     w.list = dlist;
     w.begin = begin;
@@ -818,8 +967,9 @@ int launch(tpt_ctx* c, int mode, int flags, int spp, int64_t begin, int64_t stri
         hipLaunchKernelGGL(k, dim3((unsigned)((lanes + kBlock - 1) / kBlock)), dim3(kBlock), shmem, c->stream, c->ds,
                            spp, begin, stride, count, dlist, drows, c->counters);
     } else {
-        // Shards larger than kWfChunk pixel streams run as consecutive wavefronts.
-        int rc = ensure_wf(c, std::min(count, kWfChunk));
+        // Shards larger than kWfChunk pixel streams run as consecutive chunks.
+        const int64_t chunk = std::min(count, kWfChunk), last = count - (count - 1) / kWfChunk * kWfChunk;
+        int rc = ensure_wf(c, std::max(chunk * wf_iters(chunk, spp), last * wf_iters(last, spp)));
         if (rc) return rc;
         for (int64_t c0 = 0; c0 < count; c0 += kWfChunk) {
             rc = launch_bdpt_chunk(c, spp, dlist ? 0 : begin + c0 * stride, stride, std::min(kWfChunk, count - c0),
@@ -829,22 +979,40 @@ int launch(tpt_ctx* c, int mode, int flags, int spp, int64_t begin, int64_t stri
     }
     HIP_TRY(c, hipGetLastError());
     HIP_TRY(c, hipEventRecord(c->ev1, c->stream));
+    const int64_t npix = (int64_t)c->hs.width * c->hs.height;
     if (mode == TPT_MODE_BDPT && dsplat) {
-        int64_t n = (int64_t)c->hs.width * c->hs.height * 3;
+        int64_t n = npix * 3;
         hipLaunchKernelGGL(tpt_scale_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, c->stream, dsplat, n,
                            (float)spp);
         HIP_TRY(c, hipGetLastError());
     }
+    if (st) {  // non-finite pixels of the output: listed rows, or the whole frame buffer of a shard
+        const int64_t rows = dlist ? count : npix;
+        auto grid = [](int64_t r) { return (unsigned)std::min<int64_t>(2048, (r + kBlock - 1) / kBlock); };
+        hipLaunchKernelGGL(tpt_count_nonfinite_kernel, dim3(grid(rows)), dim3(kBlock), 0, c->stream, drows, rows,
+                           c->counters + 2);
+        if (mode == TPT_MODE_BDPT && dsplat)
+            hipLaunchKernelGGL(tpt_count_nonfinite_kernel, dim3(grid(npix)), dim3(kBlock), 0, c->stream, dsplat, npix,
+                               c->counters + 3);
+        HIP_TRY(c, hipGetLastError());
+    }
     HIP_TRY(c, hipStreamSynchronize(c->stream));
+    if (mode == TPT_MODE_BDPT) {
+        int stall = 0;
+        HIP_TRY(c, hipMemcpy(&stall, c->counters + 4, sizeof(stall), hipMemcpyDeviceToHost));
+        if (stall) return fail(c, TPT_E_DEVICE, "BDPT: a gen lane timed out waiting for the previous wavefront");
+    }
     if (st) {
         float ms = 0.f;
         HIP_TRY(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
         st->kernel_ms = ms;
         st->pixels = count;
         st->samples = count * (int64_t)spp;
-        unsigned long long nb = 0;
-        HIP_TRY(c, hipMemcpy(&nb, c->counters, sizeof(nb), hipMemcpyDeviceToHost));
-        st->bounces = (int64_t)nb;
+        unsigned long long cnt[4] = {0, 0, 0, 0};
+        HIP_TRY(c, hipMemcpy(cnt, c->counters, sizeof(cnt), hipMemcpyDeviceToHost));
+        st->bounces = (int64_t)cnt[0];
+        st->nonfinite = (int64_t)cnt[2];
+        st->nonfinite_splat = (int64_t)cnt[3];
     }
     return TPT_OK;
 }
@@ -884,12 +1052,14 @@ int tpt_create(int device, tpt_ctx** out) {
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
         hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->stream3, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_start, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_gen[0], hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_gen[1], hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_fold[0], hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_fold[1], hipEventDisableTiming) != hipSuccess ||
         hipMalloc(&c->counters, sizeof(unsigned long long) * 32) != hipSuccess ||
-        hipMalloc(&c->queue, 8 * 64) != hipSuccess ||
+        hipMalloc(&c->queue, 2 * 8 * 64) != hipSuccess ||
         hipDeviceGetAttribute(&c->num_cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) {
         delete c;
         return TPT_E_DEVICE;
@@ -915,9 +1085,11 @@ void tpt_destroy(tpt_ctx* c) {
                     c->wf_mem, c->scan_tmp})
         if (p) (void)hipFree(p);
     if (c->stream2) (void)hipStreamSynchronize(c->stream2);
-    for (hipEvent_t e : {c->ev_gen[0], c->ev_gen[1], c->ev_fold[0], c->ev_fold[1]})
+    if (c->stream3) (void)hipStreamSynchronize(c->stream3);
+    for (hipEvent_t e : {c->ev_gen[0], c->ev_gen[1], c->ev_fold[0], c->ev_fold[1], c->ev_start})
         if (e) (void)hipEventDestroy(e);
     if (c->stream2) (void)hipStreamDestroy(c->stream2);
+    if (c->stream3) (void)hipStreamDestroy(c->stream3);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->stream) (void)hipStreamDestroy(c->stream);

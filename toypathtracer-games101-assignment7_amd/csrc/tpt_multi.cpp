@@ -8,9 +8,10 @@
 //     buffer on that device.  Every pixel's XorShift stream starts at ResetRandom(i+1)
 //     (:42) whichever device renders it, so the frame does not depend on n;
 //   * each device's splat buffer is already scaled by 1/spp (:59) when the reduce sums
-//     the n [rgb; splat] buffers onto the first device (ncclReduce, sum, fp32); the
-//     radiance shards are disjoint (x + 0 = x: bit-identical to one GPU) and the
-//     splats are a genuine sum, the reference's per-thread merge (:98-114).
+//     the n [rgb; splat] buffers onto the first device (ncclReduce, sum, fp32; for PT,
+//     which splats nothing, the rgb half alone); the radiance shards are disjoint
+//     (x + 0 = x: bit-identical to one GPU) and the splats are a genuine sum, the
+//     reference's per-thread merge (:98-114).
 // The devices render concurrently (one host thread each: tpt_render_device is
 // synchronous); the reduce runs on a stream per device after every render returned.
 //
@@ -24,6 +25,8 @@
 #include <algorithm>
 #include <chrono>
 #include <cstring>
+#include <exception>
+#include <new>
 #include <string>
 #include <thread>
 #include <vector>
@@ -64,6 +67,23 @@ struct Rccl {
 };
 Rccl g_rccl;
 
+// tpt_multi_last_error(NULL): why the calling thread's last tpt_multi_create failed
+// (the group does not exist then, so the reason cannot live in it).
+thread_local std::string g_create_err;
+
+// Restores the calling thread's current HIP device on every return path: the group
+// switches devices per rank, and a caller (torch) in the same thread must not find
+// itself on another GPU afterwards.
+struct DeviceGuard {
+    int dev = -1;
+    DeviceGuard() {
+        if (hipGetDevice(&dev) != hipSuccess) dev = -1;
+    }
+    ~DeviceGuard() {
+        if (dev >= 0) (void)hipSetDevice(dev);
+    }
+};
+
 }  // namespace
 
 struct tpt_multi {
@@ -101,30 +121,31 @@ void release(tpt_multi* m) {
     m->ctx.clear();
 }
 
-}  // namespace
 
-extern "C" {
+int create_fail(tpt_multi* m, int code, const std::string& why) {
+    g_create_err = why;
+    if (m) {
+        release(m);
+        delete m;
+    }
+    return code;
+}
 
-int tpt_multi_create(int ngpu, const int* devices, tpt_multi** out) {
-    if (!out) return TPT_E_INVALID;
-    *out = nullptr;
+int multi_create(int ngpu, const int* devices, tpt_multi** out) {
     int avail = 0;
-    if (hipGetDeviceCount(&avail) != hipSuccess) return TPT_E_DEVICE;
-    if (ngpu < 1 || ngpu > avail) return TPT_E_INVALID;
+    if (hipGetDeviceCount(&avail) != hipSuccess) return create_fail(nullptr, TPT_E_DEVICE, "hipGetDeviceCount failed");
+    if (ngpu < 1 || ngpu > avail)
+        return create_fail(nullptr, TPT_E_INVALID,
+                           "ngpu " + std::to_string(ngpu) + " outside 1.." + std::to_string(avail));
     tpt_multi* m = new tpt_multi();
     for (int r = 0; r < ngpu; ++r) {
         const int d = devices ? devices[r] : r;
-        if (d < 0 || d >= avail || std::count(m->dev.begin(), m->dev.end(), d)) {
-            delete m;
-            return TPT_E_INVALID;
-        }
+        if (d < 0 || d >= avail || std::count(m->dev.begin(), m->dev.end(), d))
+            return create_fail(m, TPT_E_INVALID, "bad or repeated device id " + std::to_string(d));
         m->dev.push_back(d);
     }
     std::string why;
-    if (!g_rccl.open(why)) {
-        delete m;
-        return TPT_E_UNSUPPORTED;
-    }
+    if (!g_rccl.open(why)) return create_fail(m, TPT_E_UNSUPPORTED, why);
     for (int r = 0; r < ngpu; ++r) {
         tpt_ctx* c = nullptr;
         int rc = tpt_create(m->dev[r], &c);
@@ -134,33 +155,56 @@ int tpt_multi_create(int ngpu, const int* devices, tpt_multi** out) {
                              hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess))
             rc = TPT_E_DEVICE;
         m->stream.push_back(s);
-        if (rc != TPT_OK) {
-            release(m);
-            delete m;
-            return rc;
-        }
+        if (rc != TPT_OK) return create_fail(m, rc, "device " + std::to_string(m->dev[r]) + ": context or stream");
     }
     m->comm.assign(ngpu, nullptr);
-    if (g_rccl.init_all(m->comm.data(), ngpu, m->dev.data()) != ncclSuccess) {
+    const ncclResult_t e = g_rccl.init_all(m->comm.data(), ngpu, m->dev.data());
+    if (e != ncclSuccess) {
         m->comm.assign(ngpu, nullptr);
-        release(m);
-        delete m;
-        return TPT_E_DEVICE;
+        return create_fail(m, TPT_E_DEVICE, std::string("ncclCommInitAll: ") + g_rccl.err(e));
     }
     *out = m;
+    g_create_err.clear();
     return TPT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int tpt_multi_create(int ngpu, const int* devices, tpt_multi** out) {
+    if (!out) return TPT_E_INVALID;
+    *out = nullptr;
+    DeviceGuard guard;
+    try {
+        return multi_create(ngpu, devices, out);
+    } catch (const std::bad_alloc&) {
+        g_create_err = "host allocation failed";
+        return TPT_E_ALLOC;
+    } catch (const std::exception& x) {
+        g_create_err = x.what();
+        return TPT_E_DEVICE;
+    } catch (...) {
+        g_create_err = "unknown exception";
+        return TPT_E_DEVICE;
+    }
 }
 
 void tpt_multi_destroy(tpt_multi* m) {
     if (!m) return;
+    DeviceGuard guard;
     release(m);
     delete m;
 }
 
-const char* tpt_multi_last_error(const tpt_multi* m) { return m ? m->err.c_str() : "null group"; }
+// With m == NULL: the reason the calling thread's last tpt_multi_create failed.
+const char* tpt_multi_last_error(const tpt_multi* m) { return m ? m->err.c_str() : g_create_err.c_str(); }
 
-int tpt_multi_upload_scene(tpt_multi* m, const tpt_scene_desc* d) {
-    if (!m || !d) return TPT_E_INVALID;
+}  // extern "C"
+
+namespace {
+
+int multi_upload(tpt_multi* m, const tpt_scene_desc* d) {
     m->has_scene = false;
     for (size_t r = 0; r < m->ctx.size(); ++r) {
         int rc = tpt_upload_scene(m->ctx[r], d);
@@ -184,47 +228,54 @@ int tpt_multi_upload_scene(tpt_multi* m, const tpt_scene_desc* d) {
     return TPT_OK;
 }
 
-int tpt_render_multi(tpt_multi* m, const tpt_render_params* p, float* rgb, float* splat, tpt_stats* st) {
-    if (!m || !p || !rgb) return TPT_E_INVALID;
-    if (st) std::memset(st, 0, sizeof(*st));
+int multi_render(tpt_multi* m, const tpt_render_params* p, float* rgb, float* splat, tpt_stats* st) {
     if (!m->has_scene) return mfail(m, TPT_E_NOSCENE, "no scene uploaded");
     if (p->pixel_begin != 0 || p->pixel_stride != 1)
         return mfail(m, TPT_E_INVALID, "tpt_render_multi shards the whole frame itself: pixel_begin 0, stride 1");
     const auto t0 = std::chrono::steady_clock::now();
     const int n = (int)m->dev.size();
     const int64_t nf = m->fb_floats;
+    const bool bdpt = p->mode == TPT_MODE_BDPT;
     std::vector<int> rc(n, TPT_OK);
     std::vector<tpt_stats> part(n);
-    std::vector<std::thread> th;
-    for (int r = 0; r < n; ++r) {
-        th.emplace_back([&, r]() {
-            tpt_render_params q = *p;
-            q.pixel_begin = r;  // Renderer.cpp:38: i = off; i += j
-            q.pixel_stride = n;
-            // rgb and splat are zeroed by tpt_render_device (pixels outside the shard stay 0)
-            rc[r] = tpt_render_device(m->ctx[r], &q, m->fb[r], m->fb[r] + nf, &part[r]);
-            if (rc[r] == TPT_OK && p->mode != TPT_MODE_BDPT) {
-                // PT writes no splats: zero them so the reduce sums zeros
-                if (hipSetDevice(m->dev[r]) != hipSuccess ||
-                    hipMemsetAsync(m->fb[r] + nf, 0, nf * sizeof(float), m->stream[r]) != hipSuccess)
-                    rc[r] = TPT_E_DEVICE;
+    {
+        std::vector<std::thread> th;
+        th.reserve(n);
+        try {
+            for (int r = 0; r < n; ++r) {
+                th.emplace_back([&, r]() {
+                    tpt_render_params q = *p;
+                    q.pixel_begin = r;  // Renderer.cpp:38: i = off; i += j
+                    q.pixel_stride = n;
+                    // rgb (and splat for BDPT) are zeroed by tpt_render_device: pixels
+                    // outside the shard stay 0.  PT splats nothing and its splat half is
+                    // neither written nor reduced.
+                    rc[r] = tpt_render_device(m->ctx[r], &q, m->fb[r], bdpt ? m->fb[r] + nf : nullptr, &part[r]);
+                });
             }
-        });
+        } catch (...) {  // std::system_error: join what started, then report
+            for (auto& t : th) t.join();
+            return mfail(m, TPT_E_DEVICE, "cannot start a render thread");
+        }
+        for (auto& t : th) t.join();
     }
-    for (auto& t : th) t.join();
     for (int r = 0; r < n; ++r)
         if (rc[r]) return mfail(m, rc[r], "device " + std::to_string(m->dev[r]) + ": " + tpt_last_error(m->ctx[r]));
-    // ONE collective: sum the n [rgb; splat] buffers onto the first device (Renderer.cpp:98-114).
+    // ONE collective: sum the n buffers onto the first device (Renderer.cpp:98-114):
+    // [rgb; splat] (2 W*H*3 floats) for BDPT, the rgb half alone for PT / PT-indirect.
     // With one device it is RCCL's in-place single-rank reduce (a no-op), kept so the
     // one-GPU box exercises the same code path as the 8-GPU node.
+    const size_t count = (size_t)(bdpt ? 2 * nf : nf);
     {
         if (g_rccl.group_start() != ncclSuccess) return mfail(m, TPT_E_DEVICE, "ncclGroupStart");
         ncclResult_t e = ncclSuccess;
-        for (int r = 0; r < n && e == ncclSuccess; ++r) {
-            if (hipSetDevice(m->dev[r]) != hipSuccess) return mfail(m, TPT_E_DEVICE, "hipSetDevice");
-            e = g_rccl.reduce(m->fb[r], m->fb[r], (size_t)(2 * nf), ncclFloat32, ncclSum, 0, m->comm[r], m->stream[r]);
+        bool dev_ok = true;
+        for (int r = 0; r < n && e == ncclSuccess && dev_ok; ++r) {
+            dev_ok = hipSetDevice(m->dev[r]) == hipSuccess;
+            if (dev_ok) e = g_rccl.reduce(m->fb[r], m->fb[r], count, ncclFloat32, ncclSum, 0, m->comm[r], m->stream[r]);
         }
-        const ncclResult_t e2 = g_rccl.group_end();
+        const ncclResult_t e2 = g_rccl.group_end();  // always closes the group
+        if (!dev_ok) return mfail(m, TPT_E_DEVICE, "hipSetDevice");
         if (e != ncclSuccess || e2 != ncclSuccess)
             return mfail(m, TPT_E_DEVICE, std::string("ncclReduce: ") + g_rccl.err(e != ncclSuccess ? e : e2));
     }
@@ -234,19 +285,50 @@ int tpt_render_multi(tpt_multi* m, const tpt_render_params* p, float* rgb, float
     }
     if (hipSetDevice(m->dev[0]) != hipSuccess ||
         hipMemcpy(rgb, m->fb[0], nf * sizeof(float), hipMemcpyDeviceToHost) != hipSuccess ||
-        (splat && p->mode == TPT_MODE_BDPT &&
-         hipMemcpy(splat, m->fb[0] + nf, nf * sizeof(float), hipMemcpyDeviceToHost) != hipSuccess))
+        (splat && bdpt && hipMemcpy(splat, m->fb[0] + nf, nf * sizeof(float), hipMemcpyDeviceToHost) != hipSuccess))
         return mfail(m, TPT_E_DEVICE, "copy of the reduced frame");
     if (st) {
         for (int r = 0; r < n; ++r) {
             st->pixels += part[r].pixels;
             st->samples += part[r].samples;
             st->bounces += part[r].bounces;
+            st->nonfinite += part[r].nonfinite;  // shards are disjoint
             st->kernel_ms = std::max(st->kernel_ms, part[r].kernel_ms);
         }
         st->total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     }
     return TPT_OK;
+}
+
+// No C++ exception crosses the ABI (tpt.h): map them to status codes.
+template <typename F>
+int guarded(tpt_multi* m, F&& f) {
+    try {
+        return f();
+    } catch (const std::bad_alloc&) {
+        return mfail(m, TPT_E_ALLOC, "host allocation failed");
+    } catch (const std::exception& x) {
+        return mfail(m, TPT_E_DEVICE, x.what());
+    } catch (...) {
+        return mfail(m, TPT_E_DEVICE, "unknown exception");
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+int tpt_multi_upload_scene(tpt_multi* m, const tpt_scene_desc* d) {
+    if (!m || !d) return TPT_E_INVALID;
+    DeviceGuard guard;
+    return guarded(m, [&] { return multi_upload(m, d); });
+}
+
+int tpt_render_multi(tpt_multi* m, const tpt_render_params* p, float* rgb, float* splat, tpt_stats* st) {
+    if (!m || !p || !rgb) return TPT_E_INVALID;
+    if (st) std::memset(st, 0, sizeof(*st));
+    DeviceGuard guard;
+    return guarded(m, [&] { return multi_render(m, p, rgb, splat, st); });
 }
 
 }  // extern "C"

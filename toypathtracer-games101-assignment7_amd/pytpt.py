@@ -54,7 +54,8 @@ class RenderParams(ctypes.Structure):
 
 class Stats(ctypes.Structure):
     _fields_ = [("pixels", ctypes.c_int64), ("samples", ctypes.c_int64), ("bounces", ctypes.c_int64),
-                ("kernel_ms", ctypes.c_double), ("total_ms", ctypes.c_double)]
+                ("kernel_ms", ctypes.c_double), ("total_ms", ctypes.c_double),
+                ("nonfinite", ctypes.c_int64), ("nonfinite_splat", ctypes.c_int64)]
 
 
 # Every symbol declared in include/tpt.h and include/tpt_host.h.

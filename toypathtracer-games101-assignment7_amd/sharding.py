@@ -35,6 +35,28 @@ def reduce_frame(dist, fb, dst=0):
     return fb
 
 
+def shard_model(render, ns=(2, 4, 8)):
+    """One-GPU model of the N-way split.  `render(begin, stride)` renders one shard
+    alone and returns (kernel_ms, wall_ms).  For each N every shard r = 0..N-1 is
+    rendered in turn (the frame rank r of an N-GPU run would render); the model is
+
+        T_N = max_r T(shard r of N),   eff_N = T_1 / (N * T_N)
+
+    with T_1 the whole frame's time: eff_N = 1 when the split costs nothing (the work
+    divides evenly and no per-launch cost fails to shrink).  Both the device time
+    (HIP events around the kernels) and the wall time of the synchronous call are
+    reported; the reduce is not part of the model."""
+    k1, w1 = render(0, 1)
+    out = {"full_kernel_ms": round(k1, 3), "full_wall_ms": round(w1, 3)}
+    for n in ns:
+        ks, ws = zip(*[render(r, n) for r in range(n)])
+        out["n%d" % n] = {"kernel_ms": [round(k, 3) for k in ks], "wall_ms": [round(w, 3) for w in ws],
+                          "slowest_rank": int(max(range(n), key=lambda r: ks[r])),
+                          "eff_kernel": round(k1 / (n * max(ks)), 4), "eff_wall": round(w1 / (n * max(ws)), 4),
+                          "imbalance": round(max(ks) / (sum(ks) / n), 4)}
+    return out
+
+
 def merge(rgb, splat):
     """Renderer.cpp:98-114: framebuffer[j] += splat[j] after the radiance."""
     return rgb + splat if splat is not None else rgb
