@@ -4,7 +4,8 @@ no reference source is copied.  SURVEY.md §4 item 3; VERDICT r2 "Next" #2.
 
     python tests/golden/make_frames.py [c1 c2 c4_ball c4_smooth c3 c5r ...]
 
-One file per config, tests/golden/frame_<cfg>.npz:
+One file per config, tests/golden/frame_<cfg>.npz (silver16: the reference main.cpp's
+own HEAD scene, silver boxes, PT 16 spp -- the in-reference binding's check):
 
   * PT configs (c1 = configs[0] PT 16 spp, c2 = configs[1] PT 1024 spp, c4_ball /
     c4_smooth = configs[3] PT 4096 spp): the framebuffer of the real
@@ -42,7 +43,7 @@ import frames  # noqa: E402  (tests/frames.py: the summary the tests check again
 W = H = 784
 WORKERS = int(os.environ.get("FRAME_WORKERS", "8"))
 # cfg -> (preset, mode, spp); mode 0 PathTrace, 1 BDPT
-CONFIGS = {"c1": ("standard", 0, 16), "c2": ("standard", 0, 1024), "c4_ball": ("refractive_ball", 0, 4096),
+CONFIGS = {"silver16": ("silver", 0, 16), "c1": ("standard", 0, 16), "c2": ("standard", 0, 1024), "c4_ball": ("refractive_ball", 0, 4096),
            "c4_smooth": ("smooth_dielectric", 0, 4096), "c3": ("standard", 1, 256), "c5r": ("bunny", 1, 256)}
 # 64x64 crops: the image centre, the light's corner of the ceiling, a floor/left-wall corner
 CROP_ORIGINS = np.array([[360, 360], [40, 300], [700, 60]], np.int32)  # (row, col)

@@ -15,6 +15,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/tpt.h"
@@ -158,14 +159,21 @@ TPT_D uint32_t skip_jump(uint32_t st, const uint32_t* jt, int light_draws, int n
 #endif
 constexpr int kQ = TPT_PT_LANES;
 static_assert(kQ == 1 || kQ == 2 || kQ == 4 || kQ == 8 || kQ == 16, "Q must be a power of two dividing the wave");
+#ifndef TPT_PT_SMALL_PIXELS
+// PT shards of at most this many pixel streams run 16 lanes per stream instead of
+// kQ (same-box shard model, Standard 1024 spp: 1/2, 1/4, 1/8 of the frame 24.3 /
+// 13.5 / 7.6 ms with 8 lanes, 23.7 / 12.5 / 6.9 ms with 16; the whole frame 45.3 vs
+// 45.8 ms).
+#define TPT_PT_SMALL_PIXELS 400000
+#endif
 
 #ifndef TPT_PT_DPP
 #define TPT_PT_DPP 1
 #endif
-// acc += L of lane (this + jj) for jj = J, J + 1, ... < n (n <= 8), in that order.
-template <int J>
+// acc += L of lane (this + jj) for jj = J, J + 1, ... < n (n <= Q <= 16), in that order.
+template <int J, int Q>
 TPT_D void fold_dpp(V3& acc, V3 L, int n) {
-    if constexpr (J < 8) {
+    if constexpr (J < Q && J < 16) {
         if (J < n) {
             if (J == 0) {
                 acc = acc + L;
@@ -175,21 +183,34 @@ TPT_D void fold_dpp(V3& acc, V3 L, int n) {
                 acc.y = acc.y + __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, L.y), ctrl, 0xf, 0xf, false));
                 acc.z = acc.z + __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, L.z), ctrl, 0xf, 0xf, false));
             }
-            fold_dpp<J + 1>(acc, L, n);
+            fold_dpp<J + 1, Q>(acc, L, n);
         }
     }
 }
 
+#ifndef TPT_PT_WAVETIME
+#define TPT_PT_WAVETIME 0  // diagnostics only: per-wave start / end times of the PT kernel
+#endif
+#if TPT_PT_WAVETIME
+constexpr int kWaveTimeMax = 1 << 17;
+__device__ unsigned long long tpt_wavetime[3 * kWaveTimeMax];  // start, end, hw id per wave
+#endif
+
 // kSeeded: TPT_FLAG_SAMPLE_SEED -- each sample seeds its own stream (sample_seed), so
 // no lane steps past the other lanes' samples.
-template <int kSc, bool kSeeded>
+// kQP: lanes per pixel stream (8 for a frame; 16 for shards of a frame -- half as long
+// waves, so the tail of a small grid is half as long; launch()).
+template <int kSc, bool kSeeded, int kQP>
 __global__ __launch_bounds__(kBlock, TPT_PT_MINWAVES) void tpt_pt_kernel(DScene s, int spp, int64_t begin,
                                                                         int64_t stride, int64_t count,
                                                                         const int64_t* __restrict__ list,
                                                                         float* __restrict__ out, int use_jump) {
+#if TPT_PT_WAVETIME
+    const unsigned long long wt0 = __builtin_amdgcn_s_memrealtime();
+#endif
     unsigned char* lds_free = stage_scene<kSc>(s);
     uint32_t* jt = reinterpret_cast<uint32_t*>(lds_free + kPixSlots * kBlock * sizeof(float));
-    if (!kSeeded && kQ > 2 && use_jump) {
+    if (!kSeeded && kQP > 2 && use_jump) {
         build_jump(jt, s.light_draws);
         __syncthreads();
     }
@@ -197,8 +218,8 @@ __global__ __launch_bounds__(kBlock, TPT_PT_MINWAVES) void tpt_pt_kernel(DScene 
     V3 acc = v3s(0.0f);
     {
         const int64_t gl = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-        const int64_t k = gl / kQ;  // pixel ordinal in the shard / list
-        const int q = (int)(gl % kQ);  // this lane's sample phase
+        const int64_t k = gl / kQP;  // pixel ordinal in the shard / list
+        const int q = (int)(gl % kQP);  // this lane's sample phase
         const bool on = k < count;
         const int64_t i = on ? (list ? list[k] : begin + k * stride) : 0;
         const int px = (int)(i % s.width), py = (int)(i / s.width);
@@ -217,35 +238,35 @@ __global__ __launch_bounds__(kBlock, TPT_PT_MINWAVES) void tpt_pt_kernel(DScene 
             // Only acc, rs and the loop counter stay live across the sample loop: the
             // lane's phase, the material type (parked) and the output row are
             // recomputed where they are used, so nothing spills around the loop.
-            for (int j0 = 0; j0 < spp; j0 += kQ) {
+            for (int j0 = 0; j0 < spp; j0 += kQP) {
                 unsigned ln = threadIdx.x;  // opaque: the lane's phase and shuffle base are
                 asm volatile("" : "+v"(ln));  // recomputed per round, not hoisted and spilled
-                const int qq = (int)(ln & (kQ - 1));  // == q: blocks hold whole pixels
+                const int qq = (int)(ln & (kQP - 1));  // == q: blocks hold whole pixels
                 V3 L = v3s(0.0f);
                 if (j0 + qq < spp) {
                     if (kSeeded) {
-                        const int64_t kk = ((int64_t)blockIdx.x * kBlock + ln) / kQ;
+                        const int64_t kk = ((int64_t)blockIdx.x * kBlock + ln) / kQP;
                         rs = sample_seed(list ? list[kk] : begin + kk * stride, j0 + qq);
                     }
                     L = mul(pt_sample(s, px, rs), inv);
-                    if (kQ > 1 && !kSeeded) {
+                    if (kQP > 1 && !kSeeded) {
                         const int ty = px.type(s);
-                        rs = kQ > 2 && use_jump && ty != TPT_METAL
-                                 ? skip_jump(rs, jt, s.light_draws, kQ - 1, ty == TPT_DIELETRIC)
-                                 : skip_samples(rs, ty, s.light_draws, kQ - 1);
+                        rs = kQP > 2 && use_jump && ty != TPT_METAL
+                                 ? skip_jump(rs, jt, s.light_draws, kQP - 1, ty == TPT_DIELETRIC)
+                                 : skip_samples(rs, ty, s.light_draws, kQP - 1);
                     }
                 }
-                if (kQ == 1) {
+                if (kQP == 1) {
                     acc = acc + L;
-                } else if (kQ == 8 && TPT_PT_DPP) {
+                } else if ((kQP == 8 || kQP == 16) && TPT_PT_DPP) {
                     // The fold through DPP row shifts: lane i reads L of lane i + jj of its
-                    // 16-lane row, so the first lane of each pixel (i = 0 mod 8) adds its
+                    // 16-lane row, so the first lane of each pixel (i = 0 mod kQP) adds its
                     // pixel's samples in sample order (other lanes' acc is never read).
-                    const int n = spp - j0 < kQ ? spp - j0 : kQ;
-                    fold_dpp<0>(acc, L, n);
+                    const int n = spp - j0 < kQP ? spp - j0 : kQP;
+                    fold_dpp<0, kQP>(acc, L, n);
                 } else {
                     const int base = (int)(ln & 63) - qq;  // first lane of this pixel
-                    const int n = spp - j0 < kQ ? spp - j0 : kQ;
+                    const int n = spp - j0 < kQP ? spp - j0 : kQP;
                     for (int jj = 0; jj < n; ++jj) {
                         acc.x = acc.x + __shfl(L.x, base + jj);
                         acc.y = acc.y + __shfl(L.y, base + jj);
@@ -258,13 +279,23 @@ __global__ __launch_bounds__(kBlock, TPT_PT_MINWAVES) void tpt_pt_kernel(DScene 
     unsigned tid = threadIdx.x;
     asm volatile("" : "+v"(tid));  // recomputed, not kept alive across the loop
     const int64_t gl = (int64_t)blockIdx.x * kBlock + tid;
-    const int64_t k = gl / kQ;
-    if (k < count && gl % kQ == 0) {
+    const int64_t k = gl / kQP;
+    if (k < count && gl % kQP == 0) {
         const int64_t row = list ? k : begin + k * stride;
         out[3 * row + 0] = acc.x;
         out[3 * row + 1] = acc.y;
         out[3 * row + 2] = acc.z;
     }
+#if TPT_PT_WAVETIME
+    const int wv = (int)(blockIdx.x * (kBlock / 64) + threadIdx.x / 64);
+    if (lane_id() == 0 && wv < kWaveTimeMax) {
+        tpt_wavetime[3 * wv] = wt0;
+        tpt_wavetime[3 * wv + 1] = __builtin_amdgcn_s_memrealtime();
+        // HW_REG_HW_ID1 (23) in the low word, HW_REG_XCC_ID (20, 4 bits) above it
+        tpt_wavetime[3 * wv + 2] = (unsigned long long)(unsigned)__builtin_amdgcn_s_getreg(23 | (31 << 11)) |
+                                   (unsigned long long)(unsigned)__builtin_amdgcn_s_getreg(20 | (3 << 11)) << 32;
+    }
+#endif
 }
 
 #ifndef TPT_PTI_MINWAVES
@@ -947,16 +978,21 @@ int launch(tpt_ctx* c, int mode, int flags, int spp, int64_t begin, int64_t stri
     HIP_TRY(c, hipEventRecord(c->ev0, c->stream));
     const size_t shmem = (size_t)c->ds.lds_bytes;
     if (mode == TPT_MODE_PT) {
-        const int64_t qblocks = (count * kQ + kBlock - 1) / kBlock;
+        const bool q16 = kQ < 16 && count <= TPT_PT_SMALL_PIXELS;
+        const int64_t qblocks = (count * (q16 ? 16 : kQ) + kBlock - 1) / kBlock;
         size_t pshmem = shmem + (size_t)kPixSlots * kBlock * sizeof(float);
         // The jump table only where the workgroup still fits 5 times (TPT_PT_MINWAVES) in a
         // CU's LDS.  Measured: 31,872 B per workgroup keeps 5 resident, 32,128 B does not
         // (46.4 vs 49.9 ms, Standard); consistent with 1,280-B allocation granules in 160 KB.
         const int use_jump = !seeded && TPT_PT_JUMP && pshmem + kJumpWords * 4 <= kLdsGranule * (160 * 1024 / kLdsGranule / TPT_PT_MINWAVES);
         if (use_jump) pshmem += kJumpWords * 4;
-        auto k = c->sc == 2   ? (seeded ? tpt_pt_kernel<2, true> : tpt_pt_kernel<2, false>)
-                 : c->sc == 1 ? (seeded ? tpt_pt_kernel<1, true> : tpt_pt_kernel<1, false>)
-                              : (seeded ? tpt_pt_kernel<0, true> : tpt_pt_kernel<0, false>);
+        auto pick = [&](auto q) {
+            constexpr int Q = decltype(q)::value;
+            return c->sc == 2   ? (seeded ? tpt_pt_kernel<2, true, Q> : tpt_pt_kernel<2, false, Q>)
+                   : c->sc == 1 ? (seeded ? tpt_pt_kernel<1, true, Q> : tpt_pt_kernel<1, false, Q>)
+                                : (seeded ? tpt_pt_kernel<0, true, Q> : tpt_pt_kernel<0, false, Q>);
+        };
+        auto k = q16 ? pick(std::integral_constant<int, 16>{}) : pick(std::integral_constant<int, kQ>{});
         hipLaunchKernelGGL(k, dim3((unsigned)qblocks), dim3(kBlock), pshmem, c->stream, c->ds, spp, begin, stride,
                            count, dlist, drows, use_jump);
     } else if (mode == TPT_MODE_PT_INDIRECT) {
@@ -1036,6 +1072,12 @@ int check_render_args(tpt_ctx* c, int spp, int mode, int flags = 0) {
 extern "C" {
 
 int tpt_abi_version(void) { return TPT_ABI_VERSION; }
+#if TPT_PT_WAVETIME
+// diagnostics build only: copy the PT kernel's per-wave (start, end, HW_ID) records
+int tpt_diag_wavetime(unsigned long long* host, int64_t n) {
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(tpt_wavetime), (size_t)std::min<int64_t>(n, 3 * kWaveTimeMax) * 8) == hipSuccess ? 0 : -1;
+}
+#endif
 float tpt_camera_scale(double fov) { return camera_scale(fov); }
 uint32_t tpt_sample_seed(int64_t pixel, int32_t sample) { return sample_seed(pixel, sample); }
 

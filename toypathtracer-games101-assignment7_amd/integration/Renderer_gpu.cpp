@@ -1,0 +1,140 @@
+// Renderer_gpu.cpp -- the reference-side binding: a GPU
+// Renderer::Render for yangrc1234/ToyPathTracer-GAMES101-Assignment7.  A maintainer of
+// the reference compiles this file INSTEAD of its Renderer.cpp (Renderer.cpp:68-127)
+// and links libtpt.so; every other reference source, main.cpp included, is unchanged.
+//
+// Renderer::Render keeps its signature (Renderer.hpp:11), its stdout lines
+// (Renderer.cpp:70-75, :82, :116-124, with the ray counter widened to 64 bits) and
+// its output (SaveFloatImageToJpg, SceneRenderingHelper.cpp:57-70).  The worker
+// threads (FillBufferThread, Renderer.cpp:32-63, :80-96) become one tpt_render call
+// on the scene the reference built: its objects in Scene::Add order, each
+// MeshTriangle's triangles (Triangle.hpp:89, OBJ face order), each Sphere's centre and
+// radius (Sphere.hpp:14-15) and the Material fields (Material.hpp:19-25).
+// tests/native/build_inref.sh builds it against the reference's sources and
+// tests/test_gpu_parity.py::test_in_reference_binding runs it.
+#include <chrono>
+#include <cstdio>
+#include <iostream>
+#include <map>
+#include <vector>
+
+#include "Material.hpp"
+#include "Renderer.hpp"
+#include "Scene.hpp"
+#include "SceneRenderingHelper.hpp"
+#include "Sphere.hpp"
+#include "Triangle.hpp"
+#include "global.hpp"
+#include "tpt.h"
+
+// Renderer.cpp:19 defines the triangle test's epsilon (global.hpp:11 declares it)
+const float EPSILON = 1e-4;
+
+namespace {
+
+// The reference's Scene as tpt_upload_scene's flat description.
+struct GpuScene {
+    std::vector<tpt_material> mats;
+    std::vector<tpt_object> objs;
+    std::vector<float> verts;
+    tpt_scene_desc desc{};
+};
+
+void flatten(const Scene& scene, GpuScene& g) {
+    std::map<const Material*, int> ids;
+    auto mat_id = [&](const Material* m) {
+        auto it = ids.find(m);
+        if (it != ids.end()) return it->second;
+        tpt_material t{};
+        t.type = (int)m->m_type;
+        const Vector3f* v3[] = {&m->m_emission, &m->ior_m, &m->ior_m_k, &m->Kd};
+        float* dst[] = {t.emission, t.ior_m, t.ior_m_k, t.kd};
+        for (int k = 0; k < 4; ++k) {
+            dst[k][0] = v3[k]->x;
+            dst[k][1] = v3[k]->y;
+            dst[k][2] = v3[k]->z;
+        }
+        t.ior_d = m->ior_d;
+        t.rough = m->rough;  // already converted by SetSmoothness (GGX.hpp:38-40)
+        g.mats.push_back(t);
+        return ids[m] = (int)g.mats.size() - 1;
+    };
+    for (Object* o : scene.objects) {
+        tpt_object t{};
+        t.material = mat_id(o->m);
+        if (auto* mesh = dynamic_cast<MeshTriangle*>(o)) {
+            t.kind = TPT_OBJ_MESH;
+            t.first_triangle = (int)(g.verts.size() / 9);
+            t.num_triangles = (int)mesh->triangles.size();
+            for (const Triangle& tr : mesh->triangles)
+                for (const Vector3f* v : {&tr.v0, &tr.v1, &tr.v2}) g.verts.insert(g.verts.end(), {v->x, v->y, v->z});
+        } else if (auto* sp = dynamic_cast<Sphere*>(o)) {
+            t.kind = TPT_OBJ_SPHERE;
+            t.center[0] = sp->center.x;
+            t.center[1] = sp->center.y;
+            t.center[2] = sp->center.z;
+            t.radius = sp->radius;
+        } else {
+            std::fprintf(stderr, "Renderer (GPU): unsupported object type\n");
+        }
+        g.objs.push_back(t);
+    }
+    tpt_scene_desc& d = g.desc;
+    d.width = scene.width;
+    d.height = scene.height;
+    d.fov = scene.fov;
+    d.eye[0] = scene.eyePos.x; d.eye[1] = scene.eyePos.y; d.eye[2] = scene.eyePos.z;
+    d.background[0] = scene.backgroundColor.x;
+    d.background[1] = scene.backgroundColor.y;
+    d.background[2] = scene.backgroundColor.z;
+    d.num_materials = (int)g.mats.size();
+    d.materials = g.mats.data();
+    d.num_objects = (int)g.objs.size();
+    d.objects = g.objs.data();
+    d.num_vertices = (int64_t)g.verts.size() / 3;
+    d.vertices = g.verts.data();
+}
+
+}  // namespace
+
+void Renderer::Render(std::string outputFileName, const Scene& scene, int spp, int /*thread_count*/, bool bdpt) {
+    std::cout << (bdpt ? "Tracing mode: Bidirectional Ptah Tracing" : "Tracing mode: Path tracing") << std::endl;
+    const auto start = std::chrono::system_clock::now();
+    std::cout << "SPP: " << spp << "\n";
+
+    GpuScene g;
+    flatten(scene, g);
+    const size_t n = (size_t)scene.width * scene.height;
+    std::vector<float> rgb(3 * n), splat(bdpt ? 3 * n : 0);
+    tpt_stats st{};
+    tpt_ctx* ctx = nullptr;
+    int rc = tpt_create(0, &ctx);
+    if (rc == TPT_OK) rc = tpt_upload_scene(ctx, &g.desc);
+    if (rc == TPT_OK) {
+        const tpt_render_params p{spp, bdpt ? TPT_MODE_BDPT : TPT_MODE_PT, 0, 1, 0, 0};
+        rc = tpt_render(ctx, &p, rgb.data(), bdpt ? splat.data() : nullptr, &st);
+    }
+    if (rc != TPT_OK) {
+        std::fprintf(stderr, "Renderer (GPU): libtpt error %d: %s\n", rc, ctx ? tpt_last_error(ctx) : "no device");
+        tpt_destroy(ctx);
+        return;
+    }
+    tpt_destroy(ctx);
+
+    std::vector<Vector3f> framebuffer(n);
+    for (size_t j = 0; j < n; ++j) framebuffer[j] = Vector3f(rgb[3 * j], rgb[3 * j + 1], rgb[3 * j + 2]);
+    if (bdpt) {
+        std::cout << "Tracing finished, merge emission buffer\n";
+        for (size_t j = 0; j < n; ++j) framebuffer[j] += Vector3f(splat[3 * j], splat[3 * j + 1], splat[3 * j + 2]);
+    }
+    std::cout << std::endl;
+    const auto stop = std::chrono::system_clock::now();
+    const auto ms = std::chrono::duration_cast<std::chrono::milliseconds>(stop - start).count();
+    std::cout << "Render complete: \n";
+    std::cout << "Time taken: " << std::chrono::duration_cast<std::chrono::hours>(stop - start).count() << " hours\n";
+    std::cout << "          : " << std::chrono::duration_cast<std::chrono::minutes>(stop - start).count() << " minutes\n";
+    std::cout << "          : " << std::chrono::duration_cast<std::chrono::seconds>(stop - start).count() << " seconds\n";
+    std::cout << "Rays: " << st.bounces << std::endl;
+    std::cout << "Rays Per Second: " << (ms > 0 ? (double)st.bounces / 1e3 / ms : 0.0) << "MRays" << std::endl;
+    SaveFloatImageToJpg(framebuffer, scene.width, scene.height, outputFileName.c_str());
+}
