@@ -312,12 +312,15 @@ struct WfState {
     unsigned long long* incl2;  // inclusive scan of np2
     unsigned* task;       // strategy -> item | t << 22 | s << 27 (item < kWfChunk)
     float* res;           // 3 floats per strategy, in task order
+    float* isum;          // 3 floats per item: its result (nb > 1 folds in two passes)
     // Per pixel stream: (wavefronts completed) << 32 | XorShift32 state.  Consecutive
     // wavefronts' gen kernels run concurrently (two streams): the lane that finishes
     // pixel k's samples of wavefront f publishes seq f + 1 with the state in ONE 64-bit
     // agent-scope atomic store, and gen(f + 1) starts pixel k once it reads seq f + 1.
     unsigned long long* rngseq;
     int* stall;           // set when a gen lane gave up waiting (watchdog); never in a good run
+    int conc;             // 1: consecutive wavefronts' gen kernels run concurrently (two streams)
+    int nbuf;             // wavefront buffers in rotation (this one was last used by wavefront f - nbuf)
     float* acc;           // 3 floats per pixel
     const int64_t* list;  // pixel list (or null: begin + k*stride)
     int64_t begin, stride, n;  // n: pixel streams

@@ -455,15 +455,15 @@ __global__ __launch_bounds__(kBlock, TPT_GEN_MINWAVES) void tpt_bdpt_gen_kernel(
     auto start_sample = [&]() {
         const int it = b * nn + k;
         BVert c0, c1;
-        if (batch >= 2 || b > 0) {
+        if (batch >= w.nbuf || b > 0) {
             GlobPaths P;
-            P.rec = rec_at(w.rec, batch >= 2 ? it : k, 0);
+            P.rec = rec_at(w.rec, batch >= w.nbuf ? it : k, 0);
             c0 = P.cam(0);
             c1 = P.cam(1);
         } else {
             camera_vertices(s, wf_pixel(w, k), c0, c1);
         }
-        if (batch < 2) {
+        if (batch < w.nbuf) {
             rec_store(w, 0, it, c0);
             rec_store(w, 1, it, c1);
         }
@@ -474,7 +474,7 @@ __global__ __launch_bounds__(kBlock, TPT_GEN_MINWAVES) void tpt_bdpt_gen_kernel(
     };
     bool ready = false;                 // k's stream state is in rs (its previous wavefront is done)
     bool fresh = false;                 // sample b of k starts at the top of the next step
-    uint32_t wait_t0 = 0;               // when this lane started waiting for k (low 32 bits)
+    uint32_t wait_t0 = 0;               // when this lane started waiting for k (low 32 bits | 1; 0: not yet)
     for (;;) {
         const bool need = k < 0 && !drained;
         const unsigned long long nm = __ballot(need);
@@ -489,7 +489,7 @@ __global__ __launch_bounds__(kBlock, TPT_GEN_MINWAVES) void tpt_bdpt_gen_kernel(
                     k = kk;
                     b = 0;
                     ready = false;
-                    wait_t0 = (uint32_t)__builtin_amdgcn_s_memrealtime();
+                    wait_t0 = 0;
                 } else {
                     drained = true;
                 }
@@ -501,10 +501,14 @@ __global__ __launch_bounds__(kBlock, TPT_GEN_MINWAVES) void tpt_bdpt_gen_kernel(
                 w.acc[3 * k] = 0.0f; w.acc[3 * k + 1] = 0.0f; w.acc[3 * k + 2] = 0.0f;
                 ready = true;
             } else {
-                const unsigned long long v = load_rngseq(w.rngseq + k);
+                // one gen stream: gen(f - 1) completed before this kernel started, so a
+                // plain load sees its state; two: wait for its publication
+                const unsigned long long v = w.conc ? load_rngseq(w.rngseq + k) : w.rngseq[k];
                 if ((v >> 32) == (unsigned long long)batch) {
                     rs = (uint32_t)v;
                     ready = true;
+                } else if (wait_t0 == 0) {
+                    wait_t0 = (uint32_t)__builtin_amdgcn_s_memrealtime() | 1u;  // the wait starts
                 } else if (TPT_WATCHDOG && (uint32_t)__builtin_amdgcn_s_memrealtime() - wait_t0 > kStallTicks) {
                     // watchdog: give up on k, publish it so later wavefronts do not wait
                     // too, and report it.  Its items keep older contents, which are
@@ -545,7 +549,9 @@ __global__ __launch_bounds__(kBlock, TPT_GEN_MINWAVES) void tpt_bdpt_gen_kernel(
             if (++b < w.nb) {
                 fresh = true;  // the pixel's next sample, same stream, from the next step
             } else {
-                store_rngseq(w.rngseq + k, (unsigned long long)(batch + 1) << 32 | rs);
+                const unsigned long long v = (unsigned long long)(batch + 1) << 32 | rs;
+                if (w.conc) store_rngseq(w.rngseq + k, v);
+                else w.rngseq[k] = v;
                 k = -1;
                 ready = false;
             }
@@ -644,25 +650,53 @@ __global__ __launch_bounds__(kBlock, TPT_CONN_MINWAVES) void tpt_bdpt_conn_kerne
 #ifndef TPT_FLAT_DEFAULT
 #define TPT_FLAT_DEFAULT 3  // kFlatShadow | kFlatHit; measured: BDPT 882 -> 812 ms, PT 64.0 -> 61.3 ms
 #endif
+// BDPT.cpp:289-311's `result` of item it: its t > 1 strategies in (t, s) order (t = 1
+// ones were splatted), each read from its place in the task runs -- the same positions
+// tpt_bdpt_scatter_kernel wrote.
+TPT_D V3 item_result(const WfState& w, int64_t it) {
+    const StratRange r = strat_range(w, it);
+    const int ln = r.ln, cn = w.cnt[it] & 0xffff;
+    V3 res = v3s(0.0f);  // BDPT.cpp:289 `Vector3f result;`
+    auto add = [&](int64_t g) { res = res + v3(w.res[3 * g], w.res[3 * g + 1], w.res[3 * g + 2]); };
+    for (int t = 2; t <= cn; ++t) {
+        add(r.b[0] + (t - 2));  // s = 0
+        add(r.b[2] + (t - 2));  // s = 1
+        const int64_t g1 = r.b[1] + (int64_t)(t - 2) * (ln - 1) - 2;
+        for (int sl = 2; sl <= ln; ++sl) add(g1 + sl);
+    }
+    return res;
+}
+
+// One wavefront of one iteration (nb = 1): per pixel, acc += (1/spp) * result.
 __global__ __launch_bounds__(kBlock) void tpt_bdpt_fold_kernel(WfState w, float inv) {
     const int64_t k = (int64_t)blockIdx.x * kBlock + threadIdx.x;  // pixel
     if (k >= w.n) return;
     V3 acc = v3(w.acc[3 * k], w.acc[3 * k + 1], w.acc[3 * k + 2]);
-    for (int b = 0; b < w.nb; ++b) {  // the pixel's samples in order
+    for (int b = 0; b < w.nb; ++b) acc = acc + mul(item_result(w, (int64_t)b * w.n + k), inv);  // Renderer.cpp:49
+    w.acc[3 * k] = acc.x;
+    w.acc[3 * k + 1] = acc.y;
+    w.acc[3 * k + 2] = acc.z;
+}
+
+// nb > 1 in two passes, so the strategy sums run one thread per item instead of nb
+// items per pixel thread: tpt_bdpt_isum_kernel writes every item's result, then
+// tpt_bdpt_fold_items_kernel adds a pixel's nb results in sample order
+// (Renderer.cpp:49 `fb[i] += (1.0f / spp) * BDPT(...)`, the same float ops).
+__global__ __launch_bounds__(kBlock) void tpt_bdpt_isum_kernel(WfState w) {
+    const int64_t it = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (it >= w.ni) return;
+    const V3 r = item_result(w, it);
+    w.isum[3 * it] = r.x;
+    w.isum[3 * it + 1] = r.y;
+    w.isum[3 * it + 2] = r.z;
+}
+__global__ __launch_bounds__(kBlock) void tpt_bdpt_fold_items_kernel(WfState w, float inv) {
+    const int64_t k = (int64_t)blockIdx.x * kBlock + threadIdx.x;  // pixel
+    if (k >= w.n) return;
+    V3 acc = v3(w.acc[3 * k], w.acc[3 * k + 1], w.acc[3 * k + 2]);
+    for (int b = 0; b < w.nb; ++b) {
         const int64_t it = (int64_t)b * w.n + k;
-        const StratRange r = strat_range(w, it);
-        const int ln = r.ln, cn = w.cnt[it] & 0xffff;
-        V3 res = v3s(0.0f);  // BDPT.cpp:289 `Vector3f result;`
-        // the t > 1 strategies in (t, s) order (t = 1 ones were splatted), each read from
-        // its place in the task runs -- the same positions tpt_bdpt_scatter_kernel wrote
-        auto add = [&](int64_t g) { res = res + v3(w.res[3 * g], w.res[3 * g + 1], w.res[3 * g + 2]); };
-        for (int t = 2; t <= cn; ++t) {
-            add(r.b[0] + (t - 2));  // s = 0
-            add(r.b[2] + (t - 2));  // s = 1
-            const int64_t g1 = r.b[1] + (int64_t)(t - 2) * (ln - 1) - 2;
-            for (int sl = 2; sl <= ln; ++sl) add(g1 + sl);
-        }
-        acc = acc + mul(res, inv);  // Renderer.cpp:49 `fb[i] += (1.0f / spp) * BDPT(...)`
+        acc = acc + mul(v3(w.isum[3 * it], w.isum[3 * it + 1], w.isum[3 * it + 2]), inv);
     }
     w.acc[3 * k] = acc.x;
     w.acc[3 * k + 1] = acc.y;
@@ -723,6 +757,14 @@ __global__ __launch_bounds__(kBlock) void tpt_intersect_kernel(DScene s, const f
 #define TPT_BDPT_SERIAL 0  // 1: connect / fold on the gen stream (per-kernel timing builds only)
 #endif
 
+#ifndef TPT_WF_BUFS
+#define TPT_WF_BUFS 3  // BDPT wavefront buffers in flight.  Same-box shard model, 2 / 3 / 4:
+// 1/8-frame shards Standard BDPT 0.814 / 0.849 / 0.849 of linear, bunny 0.859 / 0.900 /
+// 0.898; whole frames unchanged (bunny 256 spp 1112 / 1089 / 1091 ms)
+#endif
+constexpr int kWfBufs = TPT_WF_BUFS;
+static_assert(kWfBufs >= 2 && kWfBufs <= 4, "2 to 4 wavefront buffers");
+
 struct tpt_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -746,12 +788,12 @@ struct tpt_ctx {
     // wavefront BDPT state (sized for wf_cap pixels)
     void* wf_mem = nullptr;
     int64_t wf_cap = 0;
-    WfState wf[2]{};                  // double-buffered: gen(it+1) overlaps connect(it)
+    WfState wf[kWfBufs]{};            // kWfBufs wavefront buffers: gen(f+1..) overlaps connect(f)
     hipStream_t stream2 = nullptr;    // connect + fold
     hipStream_t stream3 = nullptr;    // gen / scan / scatter of the odd wavefronts (even ones: stream)
-    hipEvent_t ev_gen[2]{}, ev_fold[2]{}, ev_start = nullptr;
+    hipEvent_t ev_gen[kWfBufs]{}, ev_fold[kWfBufs]{}, ev_start = nullptr;
     void* scan_tmp = nullptr;         // two scratch areas: the gen streams scan concurrently
-    void* scan_tmp_g[2]{};
+    void* scan_tmp_g[2]{};            // per gen stream
     size_t scan_bytes = 0;
 };
 
@@ -809,12 +851,12 @@ int ensure_wf(tpt_ctx* c, int64_t n) {
     auto al = [](int64_t b) { return (b + 255) & ~(int64_t)255; };
     const int64_t b_rec = al(2 * kMaxLen * kRecV * n * 16), b_i = al(n * 4), b_l = al(n * 8),
                   b_own = al(n * maxs * 4), b_res = al(n * maxs * 12), b_acc = al(n * 12);
-    const int64_t per_buf = b_rec + b_i + 4 * b_l + b_own + b_res;
-    const int64_t total = 2 * per_buf + b_l + b_acc;
+    const int64_t per_buf = b_rec + b_i + 4 * b_l + b_own + b_res + b_acc;
+    const int64_t total = kWfBufs * per_buf + b_l + b_acc;
     HIP_TRY(c, hipMalloc(&c->wf_mem, total));
 
     char* p = (char*)c->wf_mem;
-    for (int b = 0; b < 2; ++b) {
+    for (int b = 0; b < kWfBufs; ++b) {
         WfState& w = c->wf[b];
         w.rec = (float4*)p; p += b_rec;
         w.cnt = (int*)p; p += b_i;
@@ -824,18 +866,20 @@ int ensure_wf(tpt_ctx* c, int64_t n) {
         w.incl2 = (unsigned long long*)p; p += b_l;
         w.task = (unsigned*)p; p += b_own;
         w.res = (float*)p; p += b_res;
+        w.isum = (float*)p; p += b_acc;
     }
-    c->wf[0].rngseq = c->wf[1].rngseq = (unsigned long long*)p; p += b_l;
+    for (int b = 0; b < kWfBufs; ++b) c->wf[b].rngseq = (unsigned long long*)p;
+    p += b_l;
     // Every item's (cnt, np, np2) starts as a valid empty sample, so a wavefront whose
     // gen watchdog fired (a lane gave up on its pixel) still scans and scatters in
     // bounds.  Per array (each < 32 MB per wavefront buffer at a frame's size), on the
     // context's stream ahead of the first launch.
-    for (int b = 0; b < 2; ++b) {
+    for (int b = 0; b < kWfBufs; ++b) {
         HIP_TRY(c, hipMemsetAsync(c->wf[b].cnt, 0, n * sizeof(int), c->stream));
         HIP_TRY(c, hipMemsetAsync(c->wf[b].np, 0, n * sizeof(unsigned long long), c->stream));
         HIP_TRY(c, hipMemsetAsync(c->wf[b].np2, 0, n * sizeof(unsigned long long), c->stream));
     }
-    c->wf[0].acc = c->wf[1].acc = (float*)p;
+    for (int b = 0; b < kWfBufs; ++b) c->wf[b].acc = (float*)p;
     const WfState& w = c->wf[0];
     size_t bytes = 0;
     HIP_TRY(c, rocprim::inclusive_scan(nullptr, bytes, w.np, w.incl, (size_t)n, rocprim::plus<unsigned long long>(),
@@ -906,7 +950,7 @@ int launch_bdpt_chunk(tpt_ctx* c, int spp, int64_t begin, int64_t stride, int64_
     // both gen streams start after everything queued so far; the pixel states and the
     // queue counters of both buffers start at 0
     HIP_TRY(c, hipMemsetAsync(c->wf[0].rngseq, 0, count * sizeof(unsigned long long), c->stream));
-    HIP_TRY(c, hipMemsetAsync(c->queue, 0, 2 * 8 * 64, c->stream));
+    HIP_TRY(c, hipMemsetAsync(c->queue, 0, kWfBufs * 8 * 64, c->stream));
     HIP_TRY(c, hipEventRecord(c->ev_start, c->stream));
     HIP_TRY(c, hipStreamWaitEvent(s2, c->ev_start, 0));
     if (gs[1] != gs[0]) HIP_TRY(c, hipStreamWaitEvent(gs[1], c->ev_start, 0));
@@ -927,7 +971,7 @@ int launch_bdpt_chunk(tpt_ctx* c, int spp, int64_t begin, int64_t stride, int64_
     const unsigned gblocks = (unsigned)std::max<int64_t>(8, gb / 8 * 8);
     const float inv = 1.0f / spp;
     for (int f = 0, it0 = 0; it0 < spp; ++f, it0 += nb) {
-        const int b = f & 1;
+        const int b = f % kWfBufs, gsi = f & 1;  // wavefront buffer, gen stream
         WfState w = c->wf[b];
         w.list = dlist;
         w.begin = begin;
@@ -937,22 +981,29 @@ int launch_bdpt_chunk(tpt_ctx* c, int spp, int64_t begin, int64_t stride, int64_
         w.ni = (int64_t)w.nb * count;
         w.bounces = c->counters;
         w.stall = reinterpret_cast<int*>(c->counters + 4);
+        w.conc = two_gen ? 1 : 0;
+        w.nbuf = kWfBufs;
         unsigned* queue = c->queue + b * 8 * 16;
         const unsigned iblocks = (unsigned)((w.ni + kBlock - 1) / kBlock);
         const unsigned cblocks = (unsigned)std::min<int64_t>(TPT_CONN_GRID, (w.ni * 24 + kBlock - 1) / kBlock + 1);
-        if (f >= 2) HIP_TRY(c, hipStreamWaitEvent(gs[b], c->ev_fold[b], 0));
-        hipLaunchKernelGGL(gen_k, dim3(gblocks), dim3(kBlock), shmem, gs[b], c->ds, w, f, queue);
+        if (f >= kWfBufs) HIP_TRY(c, hipStreamWaitEvent(gs[gsi], c->ev_fold[b], 0));
+        hipLaunchKernelGGL(gen_k, dim3(gblocks), dim3(kBlock), shmem, gs[gsi], c->ds, w, f, queue);
         size_t bytes = c->scan_bytes;
-        HIP_TRY(c, rocprim::inclusive_scan(c->scan_tmp_g[b], bytes, w.np, w.incl, (size_t)w.ni,
-                                           rocprim::plus<unsigned long long>(), gs[b]));
+        HIP_TRY(c, rocprim::inclusive_scan(c->scan_tmp_g[gsi], bytes, w.np, w.incl, (size_t)w.ni,
+                                           rocprim::plus<unsigned long long>(), gs[gsi]));
         bytes = c->scan_bytes;
-        HIP_TRY(c, rocprim::inclusive_scan(c->scan_tmp_g[b], bytes, w.np2, w.incl2, (size_t)w.ni,
-                                           rocprim::plus<unsigned long long>(), gs[b]));
-        hipLaunchKernelGGL(tpt_bdpt_scatter_kernel, dim3(iblocks), dim3(kBlock), 0, gs[b], w, queue);
-        HIP_TRY(c, hipEventRecord(c->ev_gen[b], gs[b]));
+        HIP_TRY(c, rocprim::inclusive_scan(c->scan_tmp_g[gsi], bytes, w.np2, w.incl2, (size_t)w.ni,
+                                           rocprim::plus<unsigned long long>(), gs[gsi]));
+        hipLaunchKernelGGL(tpt_bdpt_scatter_kernel, dim3(iblocks), dim3(kBlock), 0, gs[gsi], w, queue);
+        HIP_TRY(c, hipEventRecord(c->ev_gen[b], gs[gsi]));
         HIP_TRY(c, hipStreamWaitEvent(s2, c->ev_gen[b], 0));
         hipLaunchKernelGGL(conn_k, dim3(cblocks), dim3(kBlock), shmem, s2, c->ds, w, dsplat);
-        hipLaunchKernelGGL(tpt_bdpt_fold_kernel, dim3(pblocks), dim3(kBlock), 0, s2, w, inv);
+        if (w.nb == 1) {
+            hipLaunchKernelGGL(tpt_bdpt_fold_kernel, dim3(pblocks), dim3(kBlock), 0, s2, w, inv);
+        } else {
+            hipLaunchKernelGGL(tpt_bdpt_isum_kernel, dim3(iblocks), dim3(kBlock), 0, s2, w);
+            hipLaunchKernelGGL(tpt_bdpt_fold_items_kernel, dim3(pblocks), dim3(kBlock), 0, s2, w, inv);
+        }
         HIP_TRY(c, hipEventRecord(c->ev_fold[b], s2));
         if (it0 + w.nb >= spp) HIP_TRY(c, hipStreamWaitEvent(c->stream, c->ev_fold[b], 0));
     }
@@ -1096,15 +1147,18 @@ int tpt_create(int device, tpt_ctx** out) {
         hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&c->stream3, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_start, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_gen[0], hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_gen[1], hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_fold[0], hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_fold[1], hipEventDisableTiming) != hipSuccess ||
         hipMalloc(&c->counters, sizeof(unsigned long long) * 32) != hipSuccess ||
-        hipMalloc(&c->queue, 2 * 8 * 64) != hipSuccess ||
+        hipMalloc(&c->queue, kWfBufs * 8 * 64) != hipSuccess ||
         hipDeviceGetAttribute(&c->num_cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) {
-        delete c;
+        tpt_destroy(c);  // releases what was created
         return TPT_E_DEVICE;
+    }
+    for (int b = 0; b < kWfBufs; ++b) {
+        if (hipEventCreateWithFlags(&c->ev_gen[b], hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&c->ev_fold[b], hipEventDisableTiming) != hipSuccess) {
+            tpt_destroy(c);
+            return TPT_E_DEVICE;
+        }
     }
     // Fail here, not in the first launch, when this device has no code object of
     // ours (the library is built for gfx950 only; there is no fallback).
@@ -1128,8 +1182,10 @@ void tpt_destroy(tpt_ctx* c) {
         if (p) (void)hipFree(p);
     if (c->stream2) (void)hipStreamSynchronize(c->stream2);
     if (c->stream3) (void)hipStreamSynchronize(c->stream3);
-    for (hipEvent_t e : {c->ev_gen[0], c->ev_gen[1], c->ev_fold[0], c->ev_fold[1], c->ev_start})
-        if (e) (void)hipEventDestroy(e);
+    for (int b = 0; b < kWfBufs; ++b)
+        for (hipEvent_t e : {c->ev_gen[b], c->ev_fold[b]})
+            if (e) (void)hipEventDestroy(e);
+    if (c->ev_start) (void)hipEventDestroy(c->ev_start);
     if (c->stream2) (void)hipStreamDestroy(c->stream2);
     if (c->stream3) (void)hipStreamDestroy(c->stream3);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
