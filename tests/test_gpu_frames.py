@@ -74,3 +74,24 @@ def test_bdpt_frame(ctx, cfg):
     # whole-frame splat energy: one fp32 buffer of atomics here, eight per-worker
     # buffers in the reference; observed 1.4e-5 relative at 256 spp
     assert np.allclose(tot, g["splat_sum"], rtol=1e-4), (tot, g["splat_sum"])
+
+
+@pytest.mark.parametrize("n", [2, 4, 8])
+def test_pt_shards_sum_to_the_reference_frame(ctx, n):
+    """configs[1] split as an N-GPU run splits it (pixel_begin = r, pixel_stride = N,
+    Renderer.cpp:38): every shard rendered alone, the shards summed as the RCCL reduce
+    sums them, and the sum equal to the real Renderer::Render's 1024-spp frame bit for
+    bit.  Shards of a frame run 16 lanes per pixel stream instead of the whole frame's 8
+    (launch(), TPT_PT_SMALL_PIXELS), so this pins that kernel too."""
+    if not _have("c2"):
+        pytest.skip("fixture frame_c2.npz not generated")
+    g = golden("frame_c2.npz")
+    ctx.upload(pytpt.Preset("standard"))
+    tot = np.zeros((784, 784, 3), np.float32)
+    for r in range(n):
+        rgb, _, st = ctx.render(1024, pytpt.MODE_PT, begin=r, stride=n)
+        own = np.zeros(784 * 784, bool)
+        own[r::n] = True
+        assert np.all(rgb.reshape(-1, 3)[~own] == 0) and st.pixels == own.sum()
+        tot += rgb
+    check_exact(tot, g, "rgb", "standard PT 1024 spp as %d shards" % n)

@@ -164,7 +164,7 @@ static_assert(kQ == 1 || kQ == 2 || kQ == 4 || kQ == 8 || kQ == 16, "Q must be a
 // kQ (same-box shard model, Standard 1024 spp: 1/2, 1/4, 1/8 of the frame 24.3 /
 // 13.5 / 7.6 ms with 8 lanes, 23.7 / 12.5 / 6.9 ms with 16; the whole frame 45.3 vs
 // 45.8 ms).
-#define TPT_PT_SMALL_PIXELS 400000
+#define TPT_PT_SMALL_PIXELS 400000  // 32 lanes at 1/8 of the frame: 0.77 of linear vs 0.82 with 16
 #endif
 
 #ifndef TPT_PT_DPP
