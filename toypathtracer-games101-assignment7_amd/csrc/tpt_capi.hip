@@ -215,6 +215,7 @@ __global__ __launch_bounds__(kBlock, TPT_PT_MINWAVES) void tpt_pt_kernel(DScene 
         __syncthreads();
     }
     s.qs = nullptr;  // coherent rays: the per-leaf flat loops (the compacted form's code folds away)
+    s.ws = nullptr;  // and the binary walks for walk groups (no LDS left for stacks at 5 blocks/CU)
     V3 acc = v3s(0.0f);
     {
         const int64_t gl = (int64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -334,6 +335,11 @@ __global__ __launch_bounds__(kBlock, TPT_PTI_MINWAVES) void tpt_pti_kernel(DScen
 #else
     s.qs = nullptr;
 #endif
+    s.ws = nullptr;
+    if constexpr (kSc == 2) {
+        __shared__ uint16_t wst[kWalkStack * kBlock];
+        s.ws = wst;
+    }
     constexpr int kL = kSeeded ? kQ : 1;  // lanes per pixel
     const int64_t gl = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     const int64_t k = gl / kL;
@@ -434,6 +440,11 @@ __global__ __launch_bounds__(kBlock, TPT_GEN_MINWAVES) void tpt_bdpt_gen_kernel(
     stage_scene<kSc>(s);
     __shared__ QScratch qsm[kBlock / 64];  // compacted flat queries (tpt_device.h)
     s.qs = qsm;
+    s.ws = nullptr;
+    if constexpr (kSc == 2) {  // walk groups: per-lane stacks of the 4-wide walks
+        __shared__ uint16_t wst[kWalkStack * kBlock];
+        s.ws = wst;
+    }
     const int shard = blockIdx.x & 7;
     // pixel ordinals and items are < kWfChunk = 2^22: 32-bit indices in the loop
     const int nn = (int)w.n;
@@ -618,6 +629,11 @@ __global__ __launch_bounds__(kBlock, TPT_CONN_MINWAVES) void tpt_bdpt_conn_kerne
     stage_scene<kSc>(s);
     __shared__ QScratch qsm[kBlock / 64];
     s.qs = qsm;
+    s.ws = nullptr;
+    if constexpr (kSc == 2) {
+        __shared__ uint16_t wst[kWalkStack * kBlock];
+        s.ws = wst;
+    }
     const int64_t total = total_tasks(w);
     const V3 eye = v3(s.eye[0], s.eye[1], s.eye[2]);
     for (int64_t g0 = (int64_t)blockIdx.x * kBlock + (threadIdx.x & ~63); g0 < total;
@@ -740,6 +756,8 @@ __global__ __launch_bounds__(kBlock) void tpt_intersect_kernel(DScene s, const f
                                                                int cull, float* __restrict__ out) {
     __shared__ QScratch qsm[kBlock / 64];
     s.qs = qsm;
+    __shared__ uint16_t wst[kWalkStack * kBlock];
+    s.ws = wst;
     const int64_t k = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (k >= n) return;
     const float* q = rays + 6 * k;
@@ -1239,7 +1257,8 @@ int tpt_upload_scene(tpt_ctx* c, const tpt_scene_desc* d) {
            o_tris = push_array(blob, hs.tris), o_trix = push_array(blob, hs.trix), o_sph = push_array(blob, hs.sph),
            o_mats = push_array(blob, hs.mats), o_objs = push_array(blob, hs.objs),
            o_em = push_array(blob, hs.emitters), o_t = push_array(blob, hs.tnodes),
-           o_lf = push_array(blob, hs.leaves), o_gr = push_array(blob, hs.groups), o_ft = push_array(blob, hs.ftris);
+           o_lf = push_array(blob, hs.leaves), o_gr = push_array(blob, hs.groups), o_ft = push_array(blob, hs.ftris),
+           o_q4 = push_array(blob, hs.qnodes);
     if (c->blob) { (void)hipFree(c->blob); c->blob = nullptr; }
     HIP_TRY(c, hipMalloc(&c->blob, blob.size()));
     HIP_TRY(c, hipMemcpy(c->blob, blob.data(), blob.size(), hipMemcpyHostToDevice));
@@ -1260,6 +1279,7 @@ int tpt_upload_scene(tpt_ctx* c, const tpt_scene_desc* d) {
     ds.groups = (const DNode*)(b + o_gr);
     ds.ngroup = (int)hs.groups.size();
     ds.ftris = lds_full ? ds.tris : (const DTri*)(b + o_ft);
+    ds.qnodes = (const QNode4*)(b + o_q4);
     ds.lds_full = lds_full;
     ds.nmats = (int)hs.mats.size();
     ds.n_emitters = (int)hs.emitters.size();

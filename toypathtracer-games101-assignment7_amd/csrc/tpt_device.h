@@ -288,6 +288,72 @@ TPT_D bool walk_group_shadow(const DScene& s, int cur, const Ray& r, V3 lc, doub
     }
     return false;
 }
+// The same walk on the group's 4-wide tree (tpt_scene.h QNode4), for lanes with a
+// per-lane LDS stack (s.ws; the BDPT kernels).  A QNode's four entry boxes are tested
+// at once from one 128-B record, so a ray descends two binary levels per dependent
+// fetch.  Passing entries are visited in entry order -- the first at once, the others
+// from the stack -- and a leaf entry is tested when its turn comes, so the triangles
+// reached and their order are the binary walk's (the skipped binary boxes enclose the
+// entries' boxes; slab monotonicity, finite inv): closest-hit ties resolve the same.
+template <bool kShadow>
+TPT_D bool walk4(const DScene& s, int q, const Ray& r, int cull, Hit& best, V3 lc, double thr) {
+    uint16_t* st = s.ws + threadIdx.x;  // [slot][lane]
+    int sp = 0;
+    int cur = q;
+    for (;;) {
+        // a leaf: its triangle test (BVHAccel::Intersect's strict `>` fold, or the
+        // shadow answer), then the next entry -- in the same step, so a lane does one
+        // triangle and one QNode per step and the two kinds of work do not alternate
+        if (cur < 0) {
+            const int prim = -1 - cur;
+            double dist;
+            if (tri_test(s.tris[prim], r, cull, dist)) {
+                if (kShadow) {
+                    const V3 hx = r.o + mul(r.d, (float)dist);
+                    if (dot3(hx - lc, hx - lc) < thr) return true;
+                } else if (best.prim < 0 || best.dist > dist) {
+                    best.dist = dist;
+                    best.prim = prim;
+                }
+            }
+            if (sp == 0) break;
+            cur = (int)(int16_t)st[kBlock * --sp];
+        }
+        if (cur >= 0) {
+            const QNode4 n = s.qnodes[cur];
+            int held = kQNone;
+            for (int j = 3; j >= 0; --j) {
+                const bool pass = n.e[j] != kQNone && slab_hit_finite(n.bmin[0][j], n.bmin[1][j], n.bmin[2][j],
+                                                                      n.bmax[0][j], n.bmax[1][j], n.bmax[2][j], r);
+                if (pass) {
+                    if (held != kQNone) st[kBlock * sp++] = (uint16_t)held;
+                    held = n.e[j];
+                }
+            }
+            if (held != kQNone) {
+                cur = held;
+            } else {
+                if (sp == 0) break;
+                cur = (int)(int16_t)st[kBlock * --sp];
+            }
+        }
+    }
+    return false;
+}
+// A walk group's closest hit / shadow answer: the 4-wide walk where the group has a
+// 4-wide tree and the kernel gave its lanes stacks, else the threaded binary walk.
+#ifndef TPT_WALK4
+#define TPT_WALK4 1
+#endif
+TPT_D void group_closest(const DScene& s, const DNode& gn, const Ray& r, int cull, Hit& best) {
+    if (TPT_WALK4 && gn.b <= -2 && s.ws) walk4<false>(s, -2 - gn.b, r, cull, best, r.o, 0.0);
+    else walk_group_closest(s, gn.a, r, cull, best);
+}
+TPT_D bool group_shadow(const DScene& s, const DNode& gn, const Ray& r, V3 lc, double thr, int cull) {
+    Hit unused;
+    if (TPT_WALK4 && gn.b <= -2 && s.ws) return walk4<true>(s, -2 - gn.b, r, cull, unused, lc, thr);
+    return walk_group_shadow(s, gn.a, r, lc, thr, cull);
+}
 // Objects are tested first (their box is the union of their leaves' boxes, so a
 // failed object box means every leaf box of it fails): a wave skips the leaves of an
 // object no lane's ray reaches.
@@ -300,7 +366,7 @@ TPT_D Hit traverse_flat(const DScene& s, const Ray& r, int cull) {
         const bool pass = slab_hit_finite(gn.bmin[0], gn.bmin[1], gn.bmin[2], gn.bmax[0], gn.bmax[1], gn.bmax[2], r);
         if (__ballot(pass) == 0) continue;
         if (s.big && gn.b < 0) {
-            if (pass) walk_group_closest(s, gn.a, r, cull, best);
+            if (pass) group_closest(s, gn, r, cull, best);
             continue;
         }
         const int j1 = gn.a + gn.b;
@@ -330,7 +396,7 @@ TPT_D bool shadow_flat(const DScene& s, const Ray& r, V3 lc, double thr, int cul
             !sh && slab_hit_finite(gn.bmin[0], gn.bmin[1], gn.bmin[2], gn.bmax[0], gn.bmax[1], gn.bmax[2], r);
         if (__ballot(pass) == 0) continue;
         if (s.big && gn.b < 0) {
-            if (pass) sh = walk_group_shadow(s, gn.a, r, lc, thr, cull);
+            if (pass) sh = group_shadow(s, gn, r, lc, thr, cull);
             continue;
         }
         const int j1 = gn.a + gn.b;
@@ -544,7 +610,7 @@ TPT_D Hit traverse_flat_c(const DScene& s, const Ray& r, int cull) {
         if (g1 < s.ngroup) {  // a walk group
             const DNode gn = s.groups[g1];
             if (slab_hit_finite(gn.bmin[0], gn.bmin[1], gn.bmin[2], gn.bmax[0], gn.bmax[1], gn.bmax[2], r))
-                walk_group_closest(s, gn.a, r, cull, best);
+                group_closest(s, gn, r, cull, best);
             ++g1;
         }
         g0 = g1;
@@ -596,7 +662,7 @@ TPT_D bool shadow_flat_c(const DScene& s, const Ray& r, double thr, int cull) {
         if (gn.b >= 0) continue;
         const bool pass =
             !sh && slab_hit_finite(gn.bmin[0], gn.bmin[1], gn.bmin[2], gn.bmax[0], gn.bmax[1], gn.bmax[2], r);
-        if (pass) sh = walk_group_shadow(s, gn.a, r, r.o, thr, cull);
+        if (pass) sh = group_shadow(s, gn, r, r.o, thr, cull);
     }
     return sh;
 }

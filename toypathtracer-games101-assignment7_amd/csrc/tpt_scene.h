@@ -45,6 +45,25 @@ static const int32_t kMeshExit = -2;
 // (tpt_scene_build.cpp: split_walk_groups).
 static const int kFlatMaxLeaves = 64;
 
+// 4-wide walk nodes for walk groups (tpt_device.h walk4_*).  A QNode stands for a
+// binary interior node P of a mesh BVH whose box the walk has already passed; its
+// entries are P's grandchildren (or a child itself when that child is a leaf) in the
+// reference's visit order (right child first, BVH.cpp:129-132), each with its own box.
+// The binary boxes in between are not tested: for a ray with finite inv a box passing
+// implies its enclosing boxes pass (slab monotonicity, tpt_device.h), so the leaves
+// reached -- and their order -- are the reference's.  128 B: six float4 of box
+// coordinates (SoA over the four entries) and the entry codes.
+struct QNode4 {
+    float bmin[3][4];  // bmin[axis][entry]
+    float bmax[3][4];
+    int32_t e[4];      // >= 0: QNode index; < 0: -1 - primitive (a leaf); kQNone: unused slot
+    int32_t pad[4];
+};
+static const int32_t kQNone = (int32_t)0x7fffffff;
+// Per-lane LDS stack of the 4-wide walk (16-bit entries): a walk group uses the
+// 4-wide tree only when its depth d satisfies 3 d + 1 <= kWalkStack.
+static const int kWalkStack = 24;
+
 // 48 B, read as three float4: (v0, n.x) (e1, n.y) (e2, n.z) -- Triangle.hpp:46-50
 struct DTri {
     float v0[3];
@@ -104,7 +123,9 @@ struct DScene {
     const DNode* tnodes;      // threaded binary tree (stackless walks), same indices as nodes
     const DNode* leaves;      // primitive leaves in the reference's DFS order (flat queries)
     const DNode* groups;      // leaves grouped per object: box, a = first leaf, b = count;
-                              // b < 0: walk group, a = first node of the mesh walk in tnodes
+                              // b < 0: walk group, a = first node of the mesh walk in tnodes,
+                              // b <= -2: its 4-wide tree's root is qnodes[-2 - b]
+    const QNode4* qnodes;     // 4-wide trees of the walk groups
     const DTri* ftris;        // triangle of flat leaf j is ftris[leaves[j].b]
     int32_t nleaf;
     int32_t ngroup;
@@ -125,6 +146,7 @@ struct DScene {
     int32_t lds_full;   // 1: nodes + triangles + flat arrays staged; 0: only the flat arrays
     int32_t big;        // the flat list has walk groups (the kernels of small scenes fold it to 0)
     void* qs;           // device only: per-wave LDS scratch of the compacted flat queries (null: off)
+    uint16_t* ws;       // device only: per-lane LDS stacks of the 4-wide walks, [slot][lane] (null: binary walks)
 };
 
 }  // namespace tpt

@@ -133,11 +133,52 @@ static void thread_tree(HostScene& hs, int n, int after, int ntop, bool scene) {
     thread_tree(hs, src.a, after, ntop, scene);
 }
 
+// The 4-wide tree below binary node p (tpt_scene.h QNode4): its entries are p's
+// grandchildren -- or a child itself when it is a leaf -- in the reference's visit
+// order, right child first (BVH.cpp:129-132).  Returns the QNode index; `depth`
+// receives the tree's depth in QNodes.
+static int build_qtree(HostScene& hs, int p, int& depth) {
+    const int q = (int)hs.qnodes.size();
+    hs.qnodes.push_back(QNode4{});
+    std::vector<int> ent;  // binary node indices, visit order
+    const DNode& P = hs.nodes[p];
+    for (int x : {P.b, P.a}) {
+        const DNode& X = hs.nodes[x];
+        if (X.a < 0) {
+            if (X.a != kEmptyLeaf) ent.push_back(x);
+        } else {
+            ent.push_back(X.b);
+            ent.push_back(X.a);
+        }
+    }
+    int dmax = 0;
+    QNode4 Q;
+    std::memset(&Q, 0, sizeof(Q));
+    for (int j = 0; j < 4; ++j) {
+        Q.e[j] = kQNone;
+        for (int k = 0; k < 3; ++k) { Q.bmin[k][j] = 0.0f; Q.bmax[k][j] = 0.0f; }
+    }
+    for (size_t j = 0; j < ent.size(); ++j) {
+        const DNode& E = hs.nodes[ent[j]];
+        for (int k = 0; k < 3; ++k) { Q.bmin[k][j] = E.bmin[k]; Q.bmax[k][j] = E.bmax[k]; }
+        if (E.a < 0) {
+            Q.e[j] = E.a == kEmptyLeaf ? kQNone : E.a;  // -1 - prim
+        } else {
+            int d = 0;
+            Q.e[j] = build_qtree(hs, ent[j], d);
+            dmax = std::max(dmax, d);
+        }
+    }
+    hs.qnodes[q] = Q;
+    depth = dmax + 1;
+    return q;
+}
+
 // Flat queries test every listed leaf; past kFlatMaxLeaves the largest meshes leave
 // the list and become walk groups {box, a = gwalk, b = -1}: a lane whose ray passes
 // the group box (the mesh root's box) walks the mesh subtree on the threaded tree,
 // at the group's place in the DFS order, so the visit order is still the reference's.
-static void split_walk_groups(HostScene& hs, const std::vector<int>& gwalk) {
+static void split_walk_groups(HostScene& hs, const std::vector<int>& gwalk, const std::vector<int>& gnode) {
     int total = (int)hs.leaves.size();
     if (total <= kFlatMaxLeaves) return;
     std::vector<int> order(hs.groups.size());
@@ -156,6 +197,15 @@ static void split_walk_groups(HostScene& hs, const std::vector<int>& gwalk) {
         if (walk[g]) {
             G.a = gwalk[g];
             G.b = -1;
+            // 4-wide tree of the mesh below the spliced root; kept when its walk stack
+            // fits (3 pending entries per level + the current one) and its indices fit
+            // the stack's 16-bit entries
+            const size_t q0 = hs.qnodes.size();
+            int depth = 0;
+            const int qr = build_qtree(hs, gnode[g], depth);
+            const bool fits = 3 * depth + 1 <= kWalkStack && hs.qnodes.size() <= 32767 && hs.tris.size() <= 32767;
+            if (fits) G.b = -2 - qr;
+            else hs.qnodes.resize(q0);
         } else {
             const int a0 = G.a;
             G.a = (int)leaves.size();
@@ -182,6 +232,7 @@ static void build_threads(HostScene& hs, int ntop, const std::vector<int>& mesh_
     // group of one.  groups[g] = {box, a = first leaf, b = leaf count}.
     hs.groups.clear();
     std::vector<int> gwalk;  // per group: first node of its mesh walk (the root's right child), -1 if none
+    std::vector<int> gnode;  // per group: the scene node (the spliced mesh root), -1 if none
     int cur = 0, cont = kWalkEnd;
     while (cur >= 0) {
         const DNode& n = hs.tnodes[cur];
@@ -195,6 +246,7 @@ static void build_threads(HostScene& hs, int ntop, const std::vector<int>& mesh_
                 g.b = 0;
                 hs.groups.push_back(g);
                 gwalk.push_back(nxt);
+                gnode.push_back(cur);
             } else {
                 nxt = n.a;
             }
@@ -207,6 +259,7 @@ static void build_threads(HostScene& hs, int ntop, const std::vector<int>& mesh_
                 g.b = 0;
                 hs.groups.push_back(g);
                 gwalk.push_back(-1);
+                gnode.push_back(-1);
             }
             hs.leaves.push_back(l);
             hs.groups.back().b++;
@@ -218,7 +271,7 @@ static void build_threads(HostScene& hs, int ntop, const std::vector<int>& mesh_
             cur = nxt;
         }
     }
-    split_walk_groups(hs, gwalk);
+    split_walk_groups(hs, gwalk, gnode);
 }
 
 int build_host_scene(const tpt_scene_desc* d, HostScene& hs, std::string& err) {

@@ -14,6 +14,7 @@ struct HostScene {
     std::vector<DNode> leaves;  // primitive leaves in the reference's visit order (flat queries)
     std::vector<DNode> groups;  // per object: its box, first leaf (a) and leaf count (b); b < 0: walk group
     std::vector<DTri> ftris;    // flat-only LDS mode: the triangle of each flat leaf, in leaf order
+    std::vector<QNode4> qnodes; // 4-wide trees of the walk groups
     std::vector<float> node_area;
     std::vector<DTri> tris;
     std::vector<DTriX> trix;
