@@ -21,17 +21,20 @@ out = {}
 for n in (1, 8):
     ctx.render_device(1024, pytpt.MODE_PT, fb[0].data_ptr(), fb[1].data_ptr(), 0, n)  # warm
     st = ctx.render_device(1024, pytpt.MODE_PT, fb[0].data_ptr(), fb[1].data_ptr(), 0, n)
-    nw = (784 * 784 + n - 1) // n * 8 // 64
+    count = (784 * 784 + n - 1) // n
+    q = 16 if count <= 400000 else 8  # launch(): TPT_PT_SMALL_PIXELS
+    nw = (count * q + 63) // 64
     buf = np.zeros(3 * (1 << 17), np.uint64)
     assert L.tpt_diag_wavetime(ctypes.c_void_p(buf.ctypes.data), buf.size) == 0
     r = buf.reshape(-1, 3)[:nw].astype(np.int64)
     t0 = r[:, 0].min()
     s, e = (r[:, 0] - t0) / 100.0, (r[:, 1] - t0) / 100.0  # us (100 MHz counter)
     d = e - s
-    blk = d.reshape(-1, 4)
-    bspan = (e.reshape(-1, 4).max(1) - s.reshape(-1, 4).min(1))
+    nb4 = len(d) // 4 * 4
+    blk = d[:nb4].reshape(-1, 4)
+    bspan = (e[:nb4].reshape(-1, 4).max(1) - s[:nb4].reshape(-1, 4).min(1))
     xcc = (r[:, 2] >> 32) & 15
-    out["n%d" % n] = {"kernel_ms": st.kernel_ms, "waves": int(nw), "span_us": float(e.max()),
+    out["n%d" % n] = {"kernel_ms": st.kernel_ms, "waves": int(nw), "lanes_per_pixel": q, "span_us": float(e.max()),
                       "wave_us_mean": float(d.mean()), "wave_us_p50": float(np.median(d)),
                       "wave_us_p99": float(np.quantile(d, 0.99)), "wave_us_max": float(d.max()),
                       "block_span_mean": float(bspan.mean()), "block_span_max": float(bspan.max()),

@@ -1,6 +1,6 @@
 #!/usr/bin/env bash
 # On the GPU box: the rocprofv3 evidence behind bench.py's numbers for this build.
-#   scripts/profile_round.sh TAG [pt|bdpt|c5 ...]   -> gpurun_out/prof_TAG/<workload>_<pass>/
+#   scripts/profile_round.sh TAG [pt|bdpt|c5|pti|c4_ball|c4_smooth ...]   -> gpurun_out/prof_TAG/<workload>_<pass>/
 # Per workload: a kernel-trace --stats pass, then the PMC passes (one rocprofv3 run
 # each, MI355X_MICROARCH.md §rocprofv3 PMC slots: <= 8 SQ, <= 4 TCC of which
 # FETCH_SIZE takes 3 and WRITE_SIZE 2, <= 2 GRBM):
@@ -33,6 +33,8 @@ for w in $work; do
     bdpt) B="python bench.py --mode bdpt --steps 1 --warmup 0 --spp 32 --no-cpu" ;;
     c5)   B="python bench.py --mode c5 --steps 1 --warmup 0 --spp 32 --no-cpu" ;;
     pti)  B="python bench.py --mode pti --steps 1 --warmup 0 --spp 64 --no-cpu" ;;
+    c4_ball)   B="python bench.py --mode c4_ball --steps 1 --warmup 0 --spp 1024 --no-cpu" ;;
+    c4_smooth) B="python bench.py --mode c4_smooth --steps 1 --warmup 0 --spp 1024 --no-cpu" ;;
     *) echo "unknown workload $w"; exit 2 ;;
   esac
   run ${w}_kt 240 rocprofv3 --kernel-trace --stats -d "$out/${w}_kt" -o run --output-format csv -- $B

@@ -13,8 +13,9 @@ p=$src/prof_$tag
 cp "$p/valu_cost.log" "profiles/${tag}_valu_cost.jsonl"
 declare -A desc=([pt]="standard PT 1024 spp, --warmup 1 --steps 1 (2 frames)"
                  [bdpt]="standard BDPT 32 spp, 1 frame" [c5]="bunny BDPT 32 spp, 1 frame"
-                 [pti]="standard PT-indirect 64 spp, 1 frame")
-for w in pt bdpt c5 pti; do
+                 [pti]="standard PT-indirect 64 spp, 1 frame"
+                 [c4_ball]="refractive ball PT 1024 spp, 1 frame" [c4_smooth]="smooth dielectric PT 1024 spp, 1 frame")
+for w in pt bdpt c5 pti c4_ball c4_smooth; do
   [ -d "$p/${w}_kt" ] || continue
   cp "$p/${w}_kt/run_kernel_stats.csv" "profiles/${tag}_${w}_kernel_stats.csv"
   { echo "# rocprofv3 PMC, $w workload = ${desc[$w]} (scripts/profile_round.sh $tag, build $build); separate passes valu1 / valu2 / misc / fetch / write; values summed over the run's dispatches"
@@ -47,10 +48,19 @@ if [ -d "$p/pti_kt" ]; then
   python3 scripts/pmc_traffic.py standard/pti tpt_pti_kernel "$p/pti_fetch/run_counter_collection.csv" \
       "$p/pti_write/run_counter_collection.csv" --frames 0.0625 --note "build $build, 64-spp profile x 16 (profiles/${tag}_pti_pmc.txt)" > /dev/null
 fi
+for c in ball:refractive_ball smooth:smooth_dielectric; do
+  w=c4_${c%%:*}; scene=${c#*:}
+  if [ -d "$p/${w}_kt" ]; then
+    python3 scripts/valu_model.py "$p" $scene/pt $w tpt_pt_kernel --scale 4 --samples 2517630976 \
+        --note "build $build; 1024-spp profile scaled to the 4096-spp frame" --source "$(src_of $w)" > /dev/null
+    python3 scripts/pmc_traffic.py $scene/pt tpt_pt_kernel "$p/${w}_fetch/run_counter_collection.csv" \
+        "$p/${w}_write/run_counter_collection.csv" --frames 0.25 --note "build $build, 1024-spp profile x 4 (profiles/${tag}_${w}_pmc.txt)" > /dev/null
+  fi
+done
 if [ -f "$src/benchkt_$tag/run_kernel_stats.csv" ]; then
   cp "$src/benchkt_$tag/run_kernel_stats.csv" "profiles/${tag}_bench_kernel_stats.csv"
 fi
 if [ -f "$src/bench_$tag.log" ]; then
-  tail -1 "$src/bench_$tag.log" >> profiles/r02_bench_lines.jsonl
+  tail -1 "$src/bench_$tag.log" >> profiles/r03_bench_lines.jsonl
 fi
 echo "reduced $p into profiles/${tag}_*"

@@ -322,7 +322,7 @@ TPT_D bool walk4(const DScene& s, int q, const Ray& r, int cull, Hit& best, V3 l
         if (cur >= 0) {
             const QNode4 n = s.qnodes[cur];
             int held = kQNone;
-            for (int j = 3; j >= 0; --j) {
+            for (int j = kWalkW - 1; j >= 0; --j) {
                 const bool pass = n.e[j] != kQNone && slab_hit_finite(n.bmin[0][j], n.bmin[1][j], n.bmin[2][j],
                                                                       n.bmax[0][j], n.bmax[1][j], n.bmax[2][j], r);
                 if (pass) {

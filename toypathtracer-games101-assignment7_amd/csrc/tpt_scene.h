@@ -45,24 +45,29 @@ static const int32_t kMeshExit = -2;
 // (tpt_scene_build.cpp: split_walk_groups).
 static const int kFlatMaxLeaves = 64;
 
-// 4-wide walk nodes for walk groups (tpt_device.h walk4_*).  A QNode stands for a
+// Wide walk nodes for walk groups (tpt_device.h walk4).  A QNode4 stands for a
 // binary interior node P of a mesh BVH whose box the walk has already passed; its
-// entries are P's grandchildren (or a child itself when that child is a leaf) in the
-// reference's visit order (right child first, BVH.cpp:129-132), each with its own box.
-// The binary boxes in between are not tested: for a ray with finite inv a box passing
-// implies its enclosing boxes pass (slab monotonicity, tpt_device.h), so the leaves
-// reached -- and their order -- are the reference's.  128 B: six float4 of box
-// coordinates (SoA over the four entries) and the entry codes.
+// kWalkW entries are P's descendants kWalkLevels binary levels down (or a shallower
+// leaf itself) in the reference's visit order (right child first, BVH.cpp:129-132),
+// each with its own box.  The binary boxes in between are not tested: for a ray with
+// finite inv a box passing implies its enclosing boxes pass (slab monotonicity,
+// tpt_device.h), so the leaves reached -- and their order -- are the reference's.
+// Layout: the box coordinates SoA over the entries, then the entry codes.
+#ifndef TPT_WALK_LEVELS
+#define TPT_WALK_LEVELS 2  // binary levels per wide node: 2 -> 4 entries (128 B), 3 -> 8 (256 B)
+#endif
+static const int kWalkLevels = TPT_WALK_LEVELS;
+static const int kWalkW = 1 << kWalkLevels;
 struct QNode4 {
-    float bmin[3][4];  // bmin[axis][entry]
-    float bmax[3][4];
-    int32_t e[4];      // >= 0: QNode index; < 0: -1 - primitive (a leaf); kQNone: unused slot
-    int32_t pad[4];
+    float bmin[3][kWalkW];  // bmin[axis][entry]
+    float bmax[3][kWalkW];
+    int32_t e[kWalkW];      // >= 0: QNode index; < 0: -1 - primitive (a leaf); kQNone: unused slot
+    int32_t pad[kWalkW];
 };
 static const int32_t kQNone = (int32_t)0x7fffffff;
-// Per-lane LDS stack of the 4-wide walk (16-bit entries): a walk group uses the
-// 4-wide tree only when its depth d satisfies 3 d + 1 <= kWalkStack.
-static const int kWalkStack = 24;
+// Per-lane LDS stack of the wide walk (16-bit entries): a walk group uses its wide
+// tree only when its depth d satisfies (kWalkW - 1) d + 1 <= kWalkStack.
+static const int kWalkStack = kWalkLevels == 2 ? 24 : 36;
 
 // 48 B, read as three float4: (v0, n.x) (e1, n.y) (e2, n.z) -- Triangle.hpp:46-50
 struct DTri {

@@ -133,36 +133,37 @@ static void thread_tree(HostScene& hs, int n, int after, int ntop, bool scene) {
     thread_tree(hs, src.a, after, ntop, scene);
 }
 
-// The 4-wide tree below binary node p (tpt_scene.h QNode4): its entries are p's
-// grandchildren -- or a child itself when it is a leaf -- in the reference's visit
-// order, right child first (BVH.cpp:129-132).  Returns the QNode index; `depth`
-// receives the tree's depth in QNodes.
+// The wide tree below binary node p (tpt_scene.h QNode4): its entries are p's
+// descendants kWalkLevels binary levels down -- or a shallower leaf itself -- in the
+// reference's visit order, right child first (BVH.cpp:129-132).  Returns the QNode
+// index; `depth` receives the tree's depth in QNodes.
+static void wide_entries(const HostScene& hs, int x, int levels, std::vector<int>& ent) {
+    const DNode& X = hs.nodes[x];
+    if (X.a < 0) {
+        if (X.a != kEmptyLeaf) ent.push_back(x);
+    } else if (levels == 0) {
+        ent.push_back(x);
+    } else {
+        wide_entries(hs, X.b, levels - 1, ent);
+        wide_entries(hs, X.a, levels - 1, ent);
+    }
+}
 static int build_qtree(HostScene& hs, int p, int& depth) {
     const int q = (int)hs.qnodes.size();
     hs.qnodes.push_back(QNode4{});
     std::vector<int> ent;  // binary node indices, visit order
     const DNode& P = hs.nodes[p];
-    for (int x : {P.b, P.a}) {
-        const DNode& X = hs.nodes[x];
-        if (X.a < 0) {
-            if (X.a != kEmptyLeaf) ent.push_back(x);
-        } else {
-            ent.push_back(X.b);
-            ent.push_back(X.a);
-        }
-    }
+    wide_entries(hs, P.b, kWalkLevels - 1, ent);
+    wide_entries(hs, P.a, kWalkLevels - 1, ent);
     int dmax = 0;
     QNode4 Q;
     std::memset(&Q, 0, sizeof(Q));
-    for (int j = 0; j < 4; ++j) {
-        Q.e[j] = kQNone;
-        for (int k = 0; k < 3; ++k) { Q.bmin[k][j] = 0.0f; Q.bmax[k][j] = 0.0f; }
-    }
+    for (int j = 0; j < kWalkW; ++j) Q.e[j] = kQNone;
     for (size_t j = 0; j < ent.size(); ++j) {
         const DNode& E = hs.nodes[ent[j]];
         for (int k = 0; k < 3; ++k) { Q.bmin[k][j] = E.bmin[k]; Q.bmax[k][j] = E.bmax[k]; }
         if (E.a < 0) {
-            Q.e[j] = E.a == kEmptyLeaf ? kQNone : E.a;  // -1 - prim
+            Q.e[j] = E.a;  // -1 - prim
         } else {
             int d = 0;
             Q.e[j] = build_qtree(hs, ent[j], d);
@@ -197,13 +198,14 @@ static void split_walk_groups(HostScene& hs, const std::vector<int>& gwalk, cons
         if (walk[g]) {
             G.a = gwalk[g];
             G.b = -1;
-            // 4-wide tree of the mesh below the spliced root; kept when its walk stack
-            // fits (3 pending entries per level + the current one) and its indices fit
-            // the stack's 16-bit entries
+            // wide tree of the mesh below the spliced root; kept when its walk stack
+            // fits (kWalkW - 1 pending entries per level + the current one) and its
+            // indices fit the stack's 16-bit entries
             const size_t q0 = hs.qnodes.size();
             int depth = 0;
             const int qr = build_qtree(hs, gnode[g], depth);
-            const bool fits = 3 * depth + 1 <= kWalkStack && hs.qnodes.size() <= 32767 && hs.tris.size() <= 32767;
+            const bool fits = (kWalkW - 1) * depth + 1 <= kWalkStack && hs.qnodes.size() <= 32767 &&
+                              hs.tris.size() <= 32767;
             if (fits) G.b = -2 - qr;
             else hs.qnodes.resize(q0);
         } else {
