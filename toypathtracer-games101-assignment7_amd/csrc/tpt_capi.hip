@@ -166,6 +166,9 @@ static_assert(kQ == 1 || kQ == 2 || kQ == 4 || kQ == 8 || kQ == 16, "Q must be a
 // 45.8 ms).
 #define TPT_PT_SMALL_PIXELS 400000  // 32 lanes at 1/8 of the frame: 0.77 of linear vs 0.82 with 16
 #endif
+#ifndef TPT_PT_TAIL_WAVES
+#define TPT_PT_TAIL_WAVES 2  // pixel streams of the grid's 64-lane tail tier, in resident waves
+#endif
 
 #ifndef TPT_PT_DPP
 #define TPT_PT_DPP 1
@@ -198,30 +201,18 @@ __device__ unsigned long long tpt_wavetime[3 * kWaveTimeMax];  // start, end, hw
 
 // kSeeded: TPT_FLAG_SAMPLE_SEED -- each sample seeds its own stream (sample_seed), so
 // no lane steps past the other lanes' samples.
-// kQP: lanes per pixel stream (8 for a frame; 16 for shards of a frame -- half as long
-// waves, so the tail of a small grid is half as long; launch()).
+// One tier of the PT grid: pixel ordinals [k0, k1) of the shard / list with kQP lanes
+// per pixel stream, `blk` the workgroup's index within the tier.
 template <int kSc, bool kSeeded, int kQP>
-__global__ __launch_bounds__(kBlock, TPT_PT_MINWAVES) void tpt_pt_kernel(DScene s, int spp, int64_t begin,
-                                                                        int64_t stride, int64_t count,
-                                                                        const int64_t* __restrict__ list,
-                                                                        float* __restrict__ out, int use_jump) {
-#if TPT_PT_WAVETIME
-    const unsigned long long wt0 = __builtin_amdgcn_s_memrealtime();
-#endif
-    unsigned char* lds_free = stage_scene<kSc>(s);
-    uint32_t* jt = reinterpret_cast<uint32_t*>(lds_free + kPixSlots * kBlock * sizeof(float));
-    if (!kSeeded && kQP > 2 && use_jump) {
-        build_jump(jt, s.light_draws);
-        __syncthreads();
-    }
-    s.qs = nullptr;  // coherent rays: the per-leaf flat loops (the compacted form's code folds away)
-    s.ws = nullptr;  // and the binary walks for walk groups (no LDS left for stacks at 5 blocks/CU)
+TPT_D void pt_tier(const DScene& s, unsigned char* lds_free, const uint32_t* jt, int spp, int64_t begin,
+                   int64_t stride, int64_t k0, int64_t k1, int64_t blk, const int64_t* __restrict__ list,
+                   float* __restrict__ out, int use_jump) {
     V3 acc = v3s(0.0f);
     {
-        const int64_t gl = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-        const int64_t k = gl / kQP;  // pixel ordinal in the shard / list
+        const int64_t gl = blk * kBlock + threadIdx.x;
+        const int64_t k = k0 + gl / kQP;  // pixel ordinal in the shard / list
         const int q = (int)(gl % kQP);  // this lane's sample phase
-        const bool on = k < count;
+        const bool on = k < k1;
         const int64_t i = on ? (list ? list[k] : begin + k * stride) : 0;
         const int px = (int)(i % s.width), py = (int)(i / s.width);
         const V3 dir = pixel_ray(px, py, s.width, s.height, s.scale);
@@ -246,7 +237,7 @@ __global__ __launch_bounds__(kBlock, TPT_PT_MINWAVES) void tpt_pt_kernel(DScene 
                 V3 L = v3s(0.0f);
                 if (j0 + qq < spp) {
                     if (kSeeded) {
-                        const int64_t kk = ((int64_t)blockIdx.x * kBlock + ln) / kQP;
+                        const int64_t kk = k0 + (blk * kBlock + ln) / kQP;
                         rs = sample_seed(list ? list[kk] : begin + kk * stride, j0 + qq);
                     }
                     L = mul(pt_sample(s, px, rs), inv);
@@ -259,12 +250,21 @@ __global__ __launch_bounds__(kBlock, TPT_PT_MINWAVES) void tpt_pt_kernel(DScene 
                 }
                 if (kQP == 1) {
                     acc = acc + L;
-                } else if ((kQP == 8 || kQP == 16) && TPT_PT_DPP) {
+                } else if (kQP >= 8 && TPT_PT_DPP) {
                     // The fold through DPP row shifts: lane i reads L of lane i + jj of its
                     // 16-lane row, so the first lane of each pixel (i = 0 mod kQP) adds its
-                    // pixel's samples in sample order (other lanes' acc is never read).
+                    // pixel's samples in sample order (other lanes' acc is never read);
+                    // past 16 lanes the other rows' samples follow through shuffles.
                     const int n = spp - j0 < kQP ? spp - j0 : kQP;
-                    fold_dpp<0, kQP>(acc, L, n);
+                    fold_dpp<0, kQP>(acc, L, n < 16 ? n : 16);
+                    if (kQP > 16) {
+                        const int l0 = lane_id();
+                        for (int jj = 16; jj < n; ++jj) {
+                            acc.x = acc.x + __shfl(L.x, l0 + jj);
+                            acc.y = acc.y + __shfl(L.y, l0 + jj);
+                            acc.z = acc.z + __shfl(L.z, l0 + jj);
+                        }
+                    }
                 } else {
                     const int base = (int)(ln & 63) - qq;  // first lane of this pixel
                     const int n = spp - j0 < kQP ? spp - j0 : kQP;
@@ -279,14 +279,46 @@ __global__ __launch_bounds__(kBlock, TPT_PT_MINWAVES) void tpt_pt_kernel(DScene 
     }
     unsigned tid = threadIdx.x;
     asm volatile("" : "+v"(tid));  // recomputed, not kept alive across the loop
-    const int64_t gl = (int64_t)blockIdx.x * kBlock + tid;
-    const int64_t k = gl / kQP;
-    if (k < count && gl % kQP == 0) {
+    const int64_t gl = blk * kBlock + tid;
+    const int64_t k = k0 + gl / kQP;
+    if (k < k1 && gl % kQP == 0) {
         const int64_t row = list ? k : begin + k * stride;
         out[3 * row + 0] = acc.x;
         out[3 * row + 1] = acc.y;
         out[3 * row + 2] = acc.z;
     }
+}
+
+// The PT grid in two tiers: pixels [0, k_tail) with kQP lanes per pixel stream (8 for a
+// frame; 16 for shards of a frame -- half as long waves, so the tail of a small grid is
+// half as long; launch()), then pixels [k_tail, count) with kQT = 64 lanes each (one
+// wave per pixel stream, a quarter of a 16-lane wave's time).  Workgroups are
+// dispatched in order, so the short waves of the last tier are what is left to run
+// while the long ones drain: they fill the grid's tail.  A pixel's result does not
+// depend on its tier (the same samples, folded in sample order).
+constexpr int kQT = 64;
+template <int kSc, bool kSeeded, int kQP>
+__global__ __launch_bounds__(kBlock, TPT_PT_MINWAVES) void tpt_pt_kernel(DScene s, int spp, int64_t begin,
+                                                                        int64_t stride, int64_t count,
+                                                                        const int64_t* __restrict__ list,
+                                                                        float* __restrict__ out, int use_jump,
+                                                                        int64_t k_tail, int64_t b_tail) {
+#if TPT_PT_WAVETIME
+    const unsigned long long wt0 = __builtin_amdgcn_s_memrealtime();
+#endif
+    unsigned char* lds_free = stage_scene<kSc>(s);
+    uint32_t* jt = reinterpret_cast<uint32_t*>(lds_free + kPixSlots * kBlock * sizeof(float));
+    if (!kSeeded && kQP > 2 && use_jump) {
+        build_jump(jt, s.light_draws);
+        __syncthreads();
+    }
+    s.qs = nullptr;  // coherent rays: the per-leaf flat loops (the compacted form's code folds away)
+    s.ws = nullptr;  // and the binary walks for walk groups (no LDS left for stacks at 5 blocks/CU)
+    if ((int64_t)blockIdx.x < b_tail)
+        pt_tier<kSc, kSeeded, kQP>(s, lds_free, jt, spp, begin, stride, 0, k_tail, blockIdx.x, list, out, use_jump);
+    else
+        pt_tier<kSc, kSeeded, kQT>(s, lds_free, jt, spp, begin, stride, k_tail, count, blockIdx.x - b_tail, list, out,
+                                   use_jump);
 #if TPT_PT_WAVETIME
     const int wv = (int)(blockIdx.x * (kBlock / 64) + threadIdx.x / 64);
     if (lane_id() == 0 && wv < kWaveTimeMax) {
@@ -1048,7 +1080,14 @@ int launch(tpt_ctx* c, int mode, int flags, int spp, int64_t begin, int64_t stri
     const size_t shmem = (size_t)c->ds.lds_bytes;
     if (mode == TPT_MODE_PT) {
         const bool q16 = kQ < 16 && count <= TPT_PT_SMALL_PIXELS;
-        const int64_t qblocks = (count * (q16 ? 16 : kQ) + kBlock - 1) / kBlock;
+        const int qm = q16 ? 16 : kQ;
+        // the grid's last TPT_PT_TAIL_WAVES x (resident waves) pixel streams run one
+        // wave each (tpt_pt_kernel's second tier), at most a quarter of the pixels
+        const int64_t resident = (int64_t)std::max(c->num_cu, 1) * 4 * TPT_PT_MINWAVES;
+        const int64_t tail = seeded ? 0 : std::min<int64_t>(count / 4, (int64_t)TPT_PT_TAIL_WAVES * resident);
+        const int64_t k_tail = count - tail;
+        const int64_t b_tail = (k_tail * qm + kBlock - 1) / kBlock;
+        const int64_t qblocks = b_tail + (tail * kQT + kBlock - 1) / kBlock;
         size_t pshmem = shmem + (size_t)kPixSlots * kBlock * sizeof(float);
         // The jump table only where the workgroup still fits 5 times (TPT_PT_MINWAVES) in a
         // CU's LDS.  Measured: 31,872 B per workgroup keeps 5 resident, 32,128 B does not
@@ -1063,7 +1102,7 @@ int launch(tpt_ctx* c, int mode, int flags, int spp, int64_t begin, int64_t stri
         };
         auto k = q16 ? pick(std::integral_constant<int, 16>{}) : pick(std::integral_constant<int, kQ>{});
         hipLaunchKernelGGL(k, dim3((unsigned)qblocks), dim3(kBlock), pshmem, c->stream, c->ds, spp, begin, stride,
-                           count, dlist, drows, use_jump);
+                           count, dlist, drows, use_jump, k_tail, b_tail);
     } else if (mode == TPT_MODE_PT_INDIRECT) {
         const int64_t lanes = count * (seeded ? kQ : 1);
         auto k = c->sc == 2   ? (seeded ? tpt_pti_kernel<2, true> : tpt_pti_kernel<2, false>)
