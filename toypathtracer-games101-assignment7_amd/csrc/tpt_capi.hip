@@ -1307,6 +1307,7 @@ int tpt_upload_scene(tpt_ctx* c, const tpt_scene_desc* d) {
     ds.nodes = (const DNode*)(b + o_nodes);
     ds.node_area = (const float*)(b + o_area);
     ds.tris = (const DTri*)(b + o_tris);
+    ds.gtris = ds.tris;
     ds.trix = (const DTriX*)(b + o_trix);
     ds.sph = (const DSphere*)(b + o_sph);
     ds.mats = (const DMat*)(b + o_mats);

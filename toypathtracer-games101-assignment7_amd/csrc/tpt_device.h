@@ -295,6 +295,38 @@ TPT_D bool walk_group_shadow(const DScene& s, int cur, const Ray& r, V3 lc, doub
 // from the stack -- and a leaf entry is tested when its turn comes, so the triangles
 // reached and their order are the binary walk's (the skipped binary boxes enclose the
 // entries' boxes; slab monotonicity, finite inv): closest-hit ties resolve the same.
+// A QNode4's box rows and entry codes as 16-B vector loads: a by-value copy of the
+// struct came out as a dwordx3 + dword pair per row (13 VMEM instructions per node;
+// the vector memory pipeline serves a divergent load per lane address, whatever its
+// width), this is 7.
+TPT_D QNode4 load_qnode(const QNode4* p) {
+    const float4* v = reinterpret_cast<const float4*>(p);
+    QNode4 n;
+    static_assert(kWalkW == 4, "load_qnode reads 4-entry rows");
+    const float4 r0 = v[0], r1 = v[1], r2 = v[2], r3 = v[3], r4 = v[4], r5 = v[5], r6 = v[6];
+    const float4 rows[6] = {r0, r1, r2, r3, r4, r5};
+    for (int a = 0; a < 3; ++a) {
+        n.bmin[a][0] = rows[a].x; n.bmin[a][1] = rows[a].y; n.bmin[a][2] = rows[a].z; n.bmin[a][3] = rows[a].w;
+        n.bmax[a][0] = rows[3 + a].x; n.bmax[a][1] = rows[3 + a].y; n.bmax[a][2] = rows[3 + a].z; n.bmax[a][3] = rows[3 + a].w;
+    }
+    n.e[0] = __builtin_bit_cast(int32_t, r6.x); n.e[1] = __builtin_bit_cast(int32_t, r6.y);
+    n.e[2] = __builtin_bit_cast(int32_t, r6.z); n.e[3] = __builtin_bit_cast(int32_t, r6.w);
+    return n;
+}
+// A walk group's triangle through a global (address space 1) load: through the generic
+// pointer it was a flat load, which also counts against lgkmcnt, so the walk's LDS stack
+// reads waited on it.
+TPT_D DTri load_gtri(const DTri* p) {
+    typedef float F4 __attribute__((ext_vector_type(4)));
+    typedef const F4 __attribute__((address_space(1)))* GF4;
+    const GF4 v = (GF4)(const void*)p;
+    const F4 a = v[0], b = v[1], c = v[2];
+    DTri t;
+    t.v0[0] = a.x; t.v0[1] = a.y; t.v0[2] = a.z; t.nx = a.w;
+    t.e1[0] = b.x; t.e1[1] = b.y; t.e1[2] = b.z; t.ny = b.w;
+    t.e2[0] = c.x; t.e2[1] = c.y; t.e2[2] = c.z; t.nz = c.w;
+    return t;
+}
 template <bool kShadow>
 TPT_D bool walk4(const DScene& s, int q, const Ray& r, int cull, Hit& best, V3 lc, double thr) {
     uint16_t* st = s.ws + threadIdx.x;  // [slot][lane]
@@ -307,7 +339,7 @@ TPT_D bool walk4(const DScene& s, int q, const Ray& r, int cull, Hit& best, V3 l
         if (cur < 0) {
             const int prim = -1 - cur;
             double dist;
-            if (tri_test(s.tris[prim], r, cull, dist)) {
+            if (tri_test(load_gtri(s.gtris + prim), r, cull, dist)) {
                 if (kShadow) {
                     const V3 hx = r.o + mul(r.d, (float)dist);
                     if (dot3(hx - lc, hx - lc) < thr) return true;
@@ -320,7 +352,7 @@ TPT_D bool walk4(const DScene& s, int q, const Ray& r, int cull, Hit& best, V3 l
             cur = (int)(int16_t)st[kBlock * --sp];
         }
         if (cur >= 0) {
-            const QNode4 n = s.qnodes[cur];
+            const QNode4 n = load_qnode(s.qnodes + cur);
             int held = kQNone;
             for (int j = kWalkW - 1; j >= 0; --j) {
                 const bool pass = n.e[j] != kQNone && slab_hit_finite(n.bmin[0][j], n.bmin[1][j], n.bmin[2][j],

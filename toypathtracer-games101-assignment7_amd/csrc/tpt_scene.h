@@ -19,7 +19,7 @@ namespace tpt {
 
 // 32 B.  a >= 0: interior (a = left, b = right).  a < 0: leaf of primitive -1-a
 // (triangles [0, ntri), spheres [ntri, ntri+nsph)).  a == kEmptyLeaf: empty mesh.
-struct DNode {
+struct alignas(16) DNode {
     float bmin[3];
     int32_t a;
     float bmax[3];
@@ -58,19 +58,20 @@ static const int kFlatMaxLeaves = 64;
 #endif
 static const int kWalkLevels = TPT_WALK_LEVELS;
 static const int kWalkW = 1 << kWalkLevels;
-struct QNode4 {
+struct alignas(16) QNode4 {
     float bmin[3][kWalkW];  // bmin[axis][entry]
     float bmax[3][kWalkW];
     int32_t e[kWalkW];      // >= 0: QNode index; < 0: -1 - primitive (a leaf); kQNone: unused slot
     int32_t pad[kWalkW];
 };
+static_assert(sizeof(QNode4) == 32 * kWalkW, "QNode4: 16-B rows");
 static const int32_t kQNone = (int32_t)0x7fffffff;
 // Per-lane LDS stack of the wide walk (16-bit entries): a walk group uses its wide
 // tree only when its depth d satisfies (kWalkW - 1) d + 1 <= kWalkStack.
 static const int kWalkStack = kWalkLevels == 2 ? 24 : 36;
 
 // 48 B, read as three float4: (v0, n.x) (e1, n.y) (e2, n.z) -- Triangle.hpp:46-50
-struct DTri {
+struct alignas(16) DTri {
     float v0[3];
     float nx;
     float e1[3];
@@ -80,13 +81,13 @@ struct DTri {
 };
 // 32 B, only touched on light sampling / pdf paths: v1, v2 (Triangle::Sample uses
 // the original vertices, Triangle.hpp:33), area (Triangle::pdf), material.
-struct DTriX {
+struct alignas(16) DTriX {
     float v1[3];
     float area;
     float v2[3];
     int32_t mat;
 };
-struct DSphere {  // Sphere.hpp:13-15
+struct alignas(16) DSphere {  // Sphere.hpp:13-15
     float c[3];
     float r;
     float r2;
@@ -105,7 +106,7 @@ struct DMat {  // Material.hpp:19-25
     int32_t has_em;  // Material::hasEmission (Material.hpp:36-39)
     int32_t pad[2];
 };
-struct DObj {
+struct alignas(16) DObj {
     int32_t kind;         // TPT_OBJ_MESH / TPT_OBJ_SPHERE
     int32_t mat;
     int32_t root;         // mesh BVH root in nodes[] (-1 if empty)
@@ -132,6 +133,7 @@ struct DScene {
                               // b <= -2: its 4-wide tree's root is qnodes[-2 - b]
     const QNode4* qnodes;     // 4-wide trees of the walk groups
     const DTri* ftris;        // triangle of flat leaf j is ftris[leaves[j].b]
+    const DTri* gtris;        // `tris` in HBM, never re-pointed to LDS (the wide walks' global loads)
     int32_t nleaf;
     int32_t ngroup;
     int32_t flat;             // flat (all-leaves) queries: kFlatShadow | kFlatHit bits, 0 = tree walks
