@@ -313,14 +313,12 @@ TPT_D QNode4 load_qnode(const QNode4* p) {
     n.e[2] = __builtin_bit_cast(int32_t, r6.z); n.e[3] = __builtin_bit_cast(int32_t, r6.w);
     return n;
 }
-// A walk group's triangle through a global (address space 1) load: through the generic
-// pointer it was a flat load, which also counts against lgkmcnt, so the walk's LDS stack
-// reads waited on it.
+// A walk group's triangle from `gtris`, which is never re-pointed to LDS, so the
+// compiler emits global loads; through `tris` (LDS in small scenes) they were flat
+// loads, which also count against lgkmcnt, so the walk's LDS stack reads waited on them.
 TPT_D DTri load_gtri(const DTri* p) {
-    typedef float F4 __attribute__((ext_vector_type(4)));
-    typedef const F4 __attribute__((address_space(1)))* GF4;
-    const GF4 v = (GF4)(const void*)p;
-    const F4 a = v[0], b = v[1], c = v[2];
+    const float4* v = reinterpret_cast<const float4*>(p);
+    const float4 a = v[0], b = v[1], c = v[2];
     DTri t;
     t.v0[0] = a.x; t.v0[1] = a.y; t.v0[2] = a.z; t.nx = a.w;
     t.e1[0] = b.x; t.e1[1] = b.y; t.e1[2] = b.z; t.ny = b.w;
