@@ -950,10 +950,19 @@ int64_t shard_count(int64_t npix, int64_t begin, int64_t stride) {
 
 #ifndef TPT_WF_ITEMS
 // Items a BDPT wavefront aims for: a shard of n pixel streams runs
-// nb = max(1, TPT_WF_ITEMS / n) sample iterations per wavefront, so a small shard
-// (1/8 of a frame on each of 8 GPUs) launches and drains as few wavefronts as a
-// whole frame does.  Default: one 784 x 784 frame's worth.
-#define TPT_WF_ITEMS 614656
+// nb = max(1, TPT_WF_ITEMS / n) sample iterations per wavefront (at most spp /
+// TPT_WF_MIN_FRONTS), so a small shard (1/8 of a frame on each of 8 GPUs) launches and
+// drains as few wavefronts as a whole frame does.  Default: two 784 x 784 frames'
+// worth, ~24 GB of wavefront buffers.  Same-box shard model (Standard BDPT 256 spp,
+// whole frame / 1/8 shard): one frame 457.9 / 64.3 ms, two 445.6 / 61.9, three 442.5 /
+// 62.0, four 438.7 / 62.9 ms (47 GB); bunny BDPT 256 spp whole frame 940 / 933 / 928 /
+// 926 ms.
+#define TPT_WF_ITEMS 1229312
+#endif
+#ifndef TPT_WF_MIN_FRONTS
+// ... and at least this many wavefronts where spp allows (a wavefront's fill and drain
+// do not overlap with another's): 1/8 shards run 16 iterations per wavefront.
+#define TPT_WF_MIN_FRONTS 16
 #endif
 #ifndef TPT_GEN_GRID_Q
 // gen's persistent grid, in 32nds of what fits on the chip at once.  A full grid
@@ -968,8 +977,7 @@ int64_t shard_count(int64_t npix, int64_t begin, int64_t stride) {
 #endif
 int wf_iters(int64_t count, int spp) {
     const int64_t nb = std::max<int64_t>(1, std::min<int64_t>((int64_t)TPT_WF_ITEMS, kWfChunk) / std::max<int64_t>(count, 1));
-    // at least four wavefronts where spp allows, so gen(f + 1) has connect(f) to overlap
-    return (int)std::min<int64_t>(nb, std::max(1, spp / 4));
+    return (int)std::min<int64_t>(nb, std::max(1, spp / TPT_WF_MIN_FRONTS));
 }
 
 // The BDPT sample loop over `count` (<= kWfChunk) pixel streams, as wavefronts of
