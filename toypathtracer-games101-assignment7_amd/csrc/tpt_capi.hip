@@ -969,8 +969,10 @@ int64_t shard_count(int64_t npix, int64_t begin, int64_t stride) {
 // occupies every CU until the queue drains, so connect (other stream) only runs in
 // gen's tail; a third of the chip leaves room for both.  Same-box sweep, Standard
 // BDPT 256 spp / bunny BDPT 256 spp: 32 -> 601 ms / -, 8 -> 592 / 1275, 9 -> 564 /
-// 1173, 10 -> 553 / 1131, 11 -> 556 / 1108, 12 -> 567 / -, 16 -> 585 / -.
-#define TPT_GEN_GRID_Q 11
+// 1173, 10 -> 553 / 1131, 11 -> 556 / 1108, 12 -> 567 / -, 16 -> 585 / -.  Round 3,
+// wavefronts of two iterations: 10 -> 445.0 / 929.5, 11 -> 447.2 / 933.6, 12 -> 449.9 /
+// 932.6 ms.
+#define TPT_GEN_GRID_Q 10
 #endif
 #ifndef TPT_GEN2_MIN_NB
 #define TPT_GEN2_MIN_NB 2  // two gen streams when a wavefront holds >= this many iterations
@@ -1014,7 +1016,10 @@ int launch_bdpt_chunk(tpt_ctx* c, int spp, int64_t begin, int64_t stride, int64_
     if (gs[1] != gs[0]) HIP_TRY(c, hipStreamWaitEvent(gs[1], c->ev_start, 0));
     const unsigned pblocks = (unsigned)((count + kBlock - 1) / kBlock);
 #ifndef TPT_CONN_GRID
-#define TPT_CONN_GRID 8192
+#define TPT_CONN_GRID 16384  // connect's grid-stride grid, small flat scenes (Standard BDPT 256 spp: 8192 / 16384 -> 445.4 / 441.2 ms)
+#endif
+#ifndef TPT_CONN_GRID_WALK
+#define TPT_CONN_GRID_WALK 8192  // ... and scenes with walk groups (bunny BDPT 256 spp: 8192 / 16384 -> 928 / 935 ms)
 #endif
     const int gen_q = TPT_GEN_GRID_Q;
     // persistent gen grid: as many workgroups as are resident at once, a multiple of
@@ -1043,7 +1048,8 @@ int launch_bdpt_chunk(tpt_ctx* c, int spp, int64_t begin, int64_t stride, int64_
         w.nbuf = kWfBufs;
         unsigned* queue = c->queue + b * 8 * 16;
         const unsigned iblocks = (unsigned)((w.ni + kBlock - 1) / kBlock);
-        const unsigned cblocks = (unsigned)std::min<int64_t>(TPT_CONN_GRID, (w.ni * 24 + kBlock - 1) / kBlock + 1);
+        const unsigned cblocks = (unsigned)std::min<int64_t>(c->sc == 2 ? TPT_CONN_GRID_WALK : TPT_CONN_GRID,
+                                                             (w.ni * 24 + kBlock - 1) / kBlock + 1);
         if (f >= kWfBufs) HIP_TRY(c, hipStreamWaitEvent(gs[gsi], c->ev_fold[b], 0));
         hipLaunchKernelGGL(gen_k, dim3(gblocks), dim3(kBlock), shmem, gs[gsi], c->ds, w, f, queue);
         size_t bytes = c->scan_bytes;
