@@ -95,3 +95,30 @@ def test_pt_shards_sum_to_the_reference_frame(ctx, n):
         assert np.all(rgb.reshape(-1, 3)[~own] == 0) and st.pixels == own.sum()
         tot += rgb
     check_exact(tot, g, "rgb", "standard PT 1024 spp as %d shards" % n)
+
+
+@pytest.mark.parametrize("cfg", BDPT_FRAMES)
+def test_bdpt_eight_shards_sum_to_the_reference_frame(ctx, cfg):
+    """configs[2] (and configs[4]'s scene at 256 spp) split as the 8-GPU run splits it:
+    each stride-8 shard rendered alone -- at 1/8 of the frame a BDPT wavefront holds 16
+    sample iterations of the shard's pixels, on two gen streams (launch_bdpt_chunk,
+    wf_iters) -- the shards' radiance summed as the RCCL reduce sums it and equal to the
+    real Renderer::Render's radiance bit for bit; the shards' splat buffers (each scaled
+    by 1/spp, Renderer.cpp:59) summed within the splat tolerances of test_bdpt_frame."""
+    if not _have(cfg):
+        pytest.skip("fixture frame_%s.npz not generated" % cfg)
+    g = golden("frame_%s.npz" % cfg)
+    ctx.upload(pytpt.Preset(str(g["preset"])))
+    spp = int(g["spp"])
+    rgb = np.zeros((784, 784, 3), np.float32)
+    splat = np.zeros((784, 784, 3), np.float32)
+    for r in range(8):
+        a, sp, st = ctx.render(spp, pytpt.MODE_BDPT, begin=r, stride=8)
+        own = np.zeros(784 * 784, bool)
+        own[r::8] = True
+        assert np.all(a.reshape(-1, 3)[~own] == 0) and st.pixels == own.sum()
+        rgb += a
+        splat += sp
+    what = "%s BDPT %d spp as 8 shards" % (g["preset"], spp)
+    check_exact(rgb, g, "rgb", what + " radiance")
+    check_close(splat, g, "splat", what + " splats", 1e-4, 1e-4, 1e-3)
