@@ -975,7 +975,8 @@ int64_t shard_count(int64_t npix, int64_t begin, int64_t stride) {
 #define TPT_GEN_GRID_Q 10
 #endif
 #ifndef TPT_GEN2_MIN_NB
-#define TPT_GEN2_MIN_NB 2  // two gen streams when a wavefront holds >= this many iterations
+#define TPT_GEN2_MIN_NB 3  // two gen streams when a wavefront holds >= this many iterations (whole frames,
+                           // 2 iterations: one stream, bunny BDPT 256 spp 931.7 -> 919.2 ms, Standard 440.8 either way)
 #endif
 int wf_iters(int64_t count, int spp) {
     const int64_t nb = std::max<int64_t>(1, std::min<int64_t>((int64_t)TPT_WF_ITEMS, kWfChunk) / std::max<int64_t>(count, 1));
