@@ -92,6 +92,10 @@ def parse():
     ap.add_argument("--sample-seed", action="store_true",
                     help="--mode pt|pti only: per-sample seeding (TPT_FLAG_SAMPLE_SEED), a non-replay throughput mode")
     ap.add_argument("--cpu-threads", type=int, default=None)
+    ap.add_argument("--rehearse", action="store_true",
+                    help="CPU rehearsal of the N-rank plumbing (gloo, no GPU, no renderer): each rank "
+                         "writes a known pattern into its pixel shard, rank 0 checks the reduced frame; "
+                         "the line carries value null (tests/test_multiproc.py)")
     return ap.parse_args()
 
 
@@ -224,6 +228,114 @@ def hbm_model(scene, mode, kernel_ms, samples, traffic_key):
                     "so frac > 1 is cache reuse, not a violated bound; traffic = measured memory-side bytes per launch"}
 
 
+def _free_port():
+    import socket
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def spawn_ranks(a):
+    """`bench.py --gpus N` (N > 1) run without a launcher: start N ranks through
+    torch.distributed.run as a CHILD process (never an exec: this process may not
+    replace itself once anything has touched the GPU) and return its exit code; rank
+    0 prints the line.  Nothing here initialises the GPU: the visible devices are
+    counted with torch.cuda.device_count(), which on ROCm reads the device list only."""
+    import subprocess
+    if not a.rehearse:
+        import torch
+        n = torch.cuda.device_count()
+        if n < a.gpus:
+            print("bench.py: --gpus %d needs %d visible GPUs, this box has %d" % (a.gpus, a.gpus, n),
+                  file=sys.stderr, flush=True)
+            return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(a.gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC for RCCL (see README)
+    env.setdefault("OMP_NUM_THREADS", "1")
+    sys.stdout.flush()
+    return subprocess.call(cmd, env=env)
+
+
+def hbm_measured(traffic_key, kernel_ms, samples):
+    """Measured memory-side traffic of the workload (profiles/traffic.json: rocprofv3
+    FETCH_SIZE / WRITE_SIZE passes, (2 x FETCH + WRITE) per MI355X_MICROARCH.md's gfx950
+    correction) per launch, scaled to this rank's samples, over the live kernel time:
+    the fraction of the 8 TB/s HBM peak the kernels really move."""
+    t = _load_json("traffic.json").get(traffic_key)
+    model = _load_json("valu_model.json").get(traffic_key)
+    if not t or not model:
+        return None
+    b = float(t["bytes_per_launch"]) * samples / float(model["samples_per_launch"])
+    gbs = b / (kernel_ms / 1e3) / 1e9
+    return {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(gbs / HBM_PEAK_GBS, 4), "bytes_per_launch": round(b),
+            "fetch_size_kb": t["fetch_size_kb"], "write_size_kb": t["write_size_kb"],
+            "source": t.get("note"),
+            "note": "MEASURED memory-side bytes (2 x FETCH_SIZE + WRITE_SIZE, rocprofv3 PMC) / live kernel time"}
+
+
+class Rehearsal:
+    """--rehearse: the N-rank plumbing of Runner (rendezvous, shard split, the one
+    reduce onto rank 0, max-over-ranks timing, per-rank records) on the CPU over gloo,
+    with no renderer: rank r writes pixel index + 1 into its shard's pixels
+    (i = r mod N, Renderer.cpp:38) and rank 0 checks that the reduced frame holds every
+    pixel's value exactly once."""
+    W = H = 64
+
+    def __init__(self, args):
+        import torch
+        import torch.distributed as dist
+        import sharding
+        self.torch, self.dist, self.sharding, self.args = torch, dist, sharding, args
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        if self.world > 1:
+            dist.init_process_group("gloo")
+        else:
+            self.dist = None
+
+    def run(self):
+        torch = self.torch
+        npix = self.W * self.H
+        begin, stride = self.sharding.shard(self.rank, self.world)
+        want = torch.arange(1, npix + 1, dtype=torch.float32).repeat_interleave(3)
+        fb = torch.zeros(2, npix * 3)
+        ok = True
+        red_ms = []
+        t0 = time.perf_counter()
+        for _ in range(self.args.warmup + self.args.steps):
+            fb.zero_()
+            idx = torch.arange(begin, npix, stride)
+            fb[0].view(npix, 3)[idx] = (idx + 1).to(torch.float32)[:, None]
+            t1 = time.perf_counter()
+            self.sharding.reduce_frame(self.dist, fb, dst=0)
+            red_ms.append((time.perf_counter() - t1) * 1e3)
+            if self.rank == 0:
+                ok = ok and bool(torch.equal(fb[0], want)) and not fb[1].any()
+        dt = time.perf_counter() - t0
+        rec = {"rank": self.rank, "device": "cpu", "pci_bus_id": None, "kernel_ms": 0.0,
+               "reduce_ms": round(sum(red_ms) / len(red_ms), 3), "pixels": len(range(begin, npix, stride))}
+        ranks = [None] * self.world
+        if self.dist is not None:
+            self.dist.all_gather_object(ranks, rec)
+            t = torch.tensor([dt], dtype=torch.float64)
+            self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+            dt = float(t.item())
+        else:
+            ranks = [rec]
+        if self.rank == 0:
+            print(json.dumps({"metric": "rehearsal (no renderer): N-rank shard + reduce plumbing", "value": None,
+                              "unit": "Msamples/s", "n_gpus": self.world, "steps": self.args.steps,
+                              "warmup": self.args.warmup, "rehearsal": True, "reduce_check": ok,
+                              "wall_s_max_over_ranks": round(dt, 4), "ranks": ranks}), flush=True)
+        if self.dist is not None:
+            self.dist.destroy_process_group()
+        return 0 if ok else 1
+
+
 class Runner:
     def __init__(self, args):
         import torch
@@ -232,8 +344,9 @@ class Runner:
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
         local = int(os.environ.get("LOCAL_RANK", "0"))
-        if args.gpus > 1 and self.world == 1:
-            sys.exit("--gpus > 1 must be launched with torch.distributed.run (one process per GPU)")
+        if args.gpus != self.world:
+            sys.exit("bench.py: --gpus %d but WORLD_SIZE %d" % (args.gpus, self.world))
+        self.local = local
         self.dist = None
         if self.world > 1:
             import torch.distributed as dist
@@ -248,6 +361,11 @@ class Runner:
         self.ctx = pytpt.Context(torch.cuda.current_device())
         self.scene = None
         self.fb = None
+        dev = torch.cuda.current_device()
+        p = torch.cuda.get_device_properties(dev)
+        self.device_rec = {"rank": self.rank, "local_rank": local, "device": dev, "name": p.name,
+                           "pci_bus_id": "%04x:%02x:%02x" % (p.pci_domain_id, p.pci_bus_id, p.pci_device_id),
+                           "uuid": str(p.uuid)}
 
     def barrier(self):
         self.torch.cuda.synchronize()
@@ -277,13 +395,22 @@ class Runner:
         # rgb half of the buffer is summed; BDPT sums rgb and splat in one reduce.
         red = fb if mode == "bdpt" else fb[:1]
 
-        def step():
+        events = []
+
+        def step(timed=False):
             # libtpt renders on its own stream: everything torch's stream has queued on
             # fb (the zero fill, the previous step's reduce) must finish before it
             # rewrites the buffers.
             stream.synchronize()
             st = self.ctx.render_device(spp, m, fb[0].data_ptr(), fb[1].data_ptr(), begin, stride, flags)
-            self.sharding.reduce_frame(self.dist, red, dst=0)  # onto rank 0 (RCCL over xGMI)
+            if timed and self.dist is not None:  # the reduce alone, on the stream it runs on
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+                self.sharding.reduce_frame(self.dist, red, dst=0)  # onto rank 0 (RCCL over xGMI)
+                e1.record(stream)
+                events.append((e0, e1))
+            else:
+                self.sharding.reduce_frame(self.dist, red, dst=0)
             return st
 
         for _ in range(warmup):
@@ -292,13 +419,19 @@ class Runner:
         kms = []
         t0 = time.perf_counter()
         for _ in range(steps):
-            st = step()
+            st = step(timed=True)
             kms.append(st.kernel_ms)
         self.barrier()
         dt = time.perf_counter() - t0
+        ranks = None
         if self.dist is not None:
             t = torch.tensor([dt], dtype=torch.float64, device="cuda")
             self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+            rec = dict(self.device_rec, kernel_ms=round(sum(kms) / len(kms), 3),
+                       reduce_ms=round(sum(a.elapsed_time(b) for a, b in events) / len(events), 4),
+                       reduce_bytes=red.numel() * 4, wall_s=round(dt, 4), samples=st.samples)
+            ranks = [None] * self.world
+            self.dist.all_gather_object(ranks, rec)
             dt = float(t.item())
         samples = W * H * spp * steps  # all ranks together cover the frame each step
         kernel_ms = sum(kms) / len(kms)
@@ -316,8 +449,14 @@ class Runner:
                            else "1 GPU"},
                 "roofline": valu_roofline(tkey, kernel_ms, shard_samples),
                 "roofline_hbm_model": hbm_model(scene, mode, kernel_ms, shard_samples, tkey),
+                "roofline_hbm_measured": hbm_measured(tkey, kernel_ms, shard_samples),
                 "kernel_ms_per_step": round(kernel_ms, 3), "samples_per_rank_step": shard_samples,
                 "nonfinite_pixels": st.nonfinite + st.nonfinite_splat}
+        if ranks is not None:
+            line["ranks"] = ranks
+            line["distinct_devices"] = len({r["pci_bus_id"] for r in ranks})
+            # kernel time of the slowest rank: the roofline of the N-GPU step
+            line["kernel_ms_max_over_ranks"] = max(r["kernel_ms"] for r in ranks)
         return line
 
     def shard_model(self):
@@ -355,8 +494,23 @@ class Runner:
             self.dist.destroy_process_group()
 
 
+def summary(lines):
+    """Compact per-config figures, last in the line so a tail of the output shows them."""
+    out = {}
+    for k, l in lines.items():
+        rf, hm = l.get("roofline") or {}, l.get("roofline_hbm_measured") or {}
+        out[k] = {"value": l["value"], "ms": l["ms_per_step"], "kernel_ms": l["kernel_ms_per_step"],
+                  "valu_frac": rf.get("frac"), "hbm_frac_measured": hm.get("frac"),
+                  "cpu": (l.get("cpu_baseline") or {}).get("value")}
+    return out
+
+
 def main():
     a = parse()
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(a))
+    if a.rehearse:
+        sys.exit(Rehearsal(a).run())
     r = Runner(a)
     if a.shard_only:
         r.fb = r.torch.zeros(2, 784 * 784 * 3, dtype=r.torch.float32, device="cuda")
@@ -389,12 +543,17 @@ def main():
                    "per-sample seeding: sample j of pixel i seeds tpt_sample_seed(i, j)" if a.sample_seed
                    else "reference seeds pixel+1"),
                "config": head["config"], "roofline": head["roofline"],
-               "roofline_hbm_model": head["roofline_hbm_model"], "cpu_baseline": head.get("cpu_baseline"),
+               "roofline_hbm_model": head["roofline_hbm_model"],
+               "roofline_hbm_measured": head["roofline_hbm_measured"], "cpu_baseline": head.get("cpu_baseline"),
                "kernel_ms_per_step": head["kernel_ms_per_step"], "nonfinite_pixels": head["nonfinite_pixels"]}
+        for f in ("ranks", "distinct_devices", "kernel_ms_max_over_ranks"):
+            if f in head:
+                out[f] = head[f]
         for k in keys[1:]:
             out[k] = lines[k]
         if shard_model is not None:
             out["shard_model"] = shard_model
+        out["summary"] = summary(lines)
         print(json.dumps(out), flush=True)
     r.close()
 

@@ -44,7 +44,15 @@ W = H = 784
 WORKERS = int(os.environ.get("FRAME_WORKERS", "8"))
 # cfg -> (preset, mode, spp); mode 0 PathTrace, 1 BDPT
 CONFIGS = {"silver16": ("silver", 0, 16), "c1": ("standard", 0, 16), "c2": ("standard", 0, 1024), "c4_ball": ("refractive_ball", 0, 4096),
-           "c4_smooth": ("smooth_dielectric", 0, 4096), "c3": ("standard", 1, 256), "c5r": ("bunny", 1, 256)}
+           "c4_smooth": ("smooth_dielectric", 0, 4096), "c3": ("standard", 1, 256), "c5r": ("bunny", 1, 256),
+           "c5": ("bunny", 1, 4096)}
+# BDPT configs made through the per-pixel route alone: configs[4] at its own 4096 spp takes
+# ~3 h of the container's 8 cores per route, and c5r already checks at 256 spp that the
+# per-pixel route and Renderer::Render agree on this scene
+TRACE_ONLY = {"c5"}
+# chunked, resumable per-pixel route for long configs: chunk c holds pixels i = c (mod CHUNKS)
+CHUNKS = {"c5": 32}
+CACHE = os.path.join(os.path.dirname(os.path.dirname(HERE)), ".frame_cache")
 # 64x64 crops: the image centre, the light's corner of the ceiling, a floor/left-wall corner
 CROP_ORIGINS = np.array([[360, 360], [40, 300], [700, 60]], np.int32)  # (row, col)
 
@@ -65,18 +73,36 @@ def _trace_worker(args):
     return rgb, splat
 
 
-def trace_frame(preset, mode, spp):
-    """The whole frame through ref_trace_pixels, pixels dealt i = w (mod WORKERS)."""
+def trace_frame(preset, mode, spp, chunks=1, tag=None):
+    """The whole frame through ref_trace_pixels, pixels dealt i = w (mod WORKERS).
+    With chunks > 1 the frame is traced as `chunks` interleaved pixel sets, each saved
+    under .frame_cache/ when done so an interrupted run resumes; the splat buffers are
+    summed in chunk order, then worker order."""
     allpix = np.arange(W * H, dtype=np.int64)
-    jobs = [(preset, mode, spp, allpix[w::WORKERS]) for w in range(WORKERS)]
-    ctx = mp.get_context("spawn")
-    with ctx.Pool(WORKERS) as pool:
-        res = pool.map(_trace_worker, jobs)
     rgb = np.zeros((W * H, 3), np.float32)
     splat = np.zeros((H, W, 3), np.float32)
-    for w, (r, s) in enumerate(res):
-        rgb[w::WORKERS] = r
-        splat += s
+    ctx = mp.get_context("spawn")
+    with ctx.Pool(WORKERS) as pool:
+        for c in range(chunks):
+            pix = allpix[c::chunks]
+            path = os.path.join(CACHE, "%s_%d_of_%d.npz" % (tag, c, chunks)) if chunks > 1 else None
+            if path and os.path.exists(path):
+                z = np.load(path)
+                rgb[pix], s = z["rgb"], z["splat"]
+            else:
+                t0 = time.time()
+                res = pool.map(_trace_worker, [(preset, mode, spp, pix[w::WORKERS]) for w in range(WORKERS)])
+                r = np.zeros((len(pix), 3), np.float32)
+                s = np.zeros((H, W, 3), np.float32)
+                for w, (rw, sw) in enumerate(res):
+                    r[w::WORKERS] = rw
+                    s += sw
+                rgb[pix] = r
+                if path:
+                    os.makedirs(CACHE, exist_ok=True)
+                    np.savez(path, rgb=r, splat=s)
+                    print("%s chunk %d/%d in %.0f s" % (tag, c + 1, chunks, time.time() - t0), flush=True)
+            splat += s
     return rgb.reshape(H, W, 3), splat
 
 
@@ -90,10 +116,16 @@ def make(cfg):
         img = Reference(preset).render(0, spp, threads=WORKERS)
         out.update(frame_summary(img, "rgb"))
     else:
-        rgb, splat = trace_frame(preset, mode, spp)
+        rgb, splat = trace_frame(preset, mode, spp, CHUNKS.get(cfg, 1), cfg)
         out.update(frame_summary(rgb, "rgb"))
         out.update(frame_blocks(splat, "splat"))
         out["splat_sum"] = splat.astype(np.float64).sum((0, 1))
+        if cfg in TRACE_ONLY:
+            out["trace_only"] = np.int32(1)
+            np.savez_compressed(os.path.join(HERE, "frame_%s.npz" % cfg), **out)
+            print("%s (%s mode %d spp %d, per-pixel route only) done in %.0f s" % (cfg, preset, mode, spp,
+                                                                                 time.time() - t0), flush=True)
+            return
         render = Reference(preset).render(1, spp, threads=WORKERS)
         out.update(frame_blocks(render, "render"))
         # the two routes: Render = radiance + per-thread splat buffers merged in thread order
