@@ -269,7 +269,12 @@ TPT_D void splat_wave(const DScene& s, bool want, V3 light, V3 cam, V3 value, fl
 // GenerateCameraPath's v0/v1 (BDPT.cpp:41-59): identical for every sample of a pixel.
 TPT_D void camera_vertices(const DScene& s, int64_t i, BVert& c0, BVert& c1) {
     const int px = (int)(i % s.width), py = (int)(i / s.width);
-    const V3 dir = pixel_ray(px, py, s.width, s.height, s.scale);
+    // opaque copies: the f64 conversions of width, height, aspect and scale are made
+    // here, not hoisted out of gen's persistent loop and spilled across it
+    int w = s.width, h = s.height;
+    float sc = s.scale;
+    asm volatile("" : "+v"(w), "+v"(h), "+v"(sc));
+    const V3 dir = pixel_ray(px, py, w, h, sc);
     const V3 eye = v3(s.eye[0], s.eye[1], s.eye[2]);
     c0.x = eye; c0.N = v3s(0.0f); c0.type = T_CAM; c0.prim = -1; c0.mat = -1;
     c0.pdf = kCamZeroPdf; c0.alpha = v3s(1.0f); c0.q1 = c0.q8 = 0.0f;
@@ -319,6 +324,9 @@ struct WfState {
     // agent-scope atomic store, and gen(f + 1) starts pixel k once it reads seq f + 1.
     unsigned long long* rngseq;
     int* stall;           // set when a gen lane gave up waiting (watchdog); never in a good run
+    unsigned stall_ticks; // the watchdog's limit (100 MHz real-time counter ticks)
+    int drop_k;           // diagnostics builds (TPT_DIAG_HOOKS): pixel ordinal whose wavefront-1
+                          // publication gen skips, to drive the watchdog path; -1 otherwise
     int conc;             // 1: consecutive wavefronts' gen kernels run concurrently (two streams)
     int nbuf;             // wavefront buffers in rotation (this one was last used by wavefront f - nbuf)
     float* acc;           // 3 floats per pixel

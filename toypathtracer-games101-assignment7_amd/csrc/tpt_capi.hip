@@ -460,11 +460,22 @@ __global__ __launch_bounds__(kBlock, TPT_PTI_MINWAVES) void tpt_pti_kernel(DScen
 #define TPT_STALL_TICKS 2000000000u  // 20 s at 100 MHz (32-bit differences wrap at 42 s)
 #endif
 constexpr uint32_t kStallTicks = TPT_STALL_TICKS;
-TPT_D unsigned long long load_rngseq(const unsigned long long* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#ifndef TPT_DIAG_HOOKS
+// 1: diagnostics build (libtpt_diag.so, tests only): each BDPT render reads
+// TPT_DIAG_DROP_PUBLISH (a pixel ordinal whose stream state gen(1) does not publish, so
+// gen(2) waits on it until the watchdog fires) and TPT_DIAG_STALL_TICKS (the watchdog's
+// limit) from the environment.  The production library has neither.
+#define TPT_DIAG_HOOKS 0
+#endif
+// The base pointer passes through an opaque SGPR copy at each use, so the compiler does
+// not keep a VGPR copy of it alive (and spilled) across gen's persistent loop.
+TPT_D unsigned long long load_rngseq(const unsigned long long* base, int k) {
+    asm volatile("" : "+s"(base));
+    return __hip_atomic_load(base + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-TPT_D void store_rngseq(unsigned long long* p, unsigned long long v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+TPT_D void store_rngseq(unsigned long long* base, int k, unsigned long long v) {
+    asm volatile("" : "+s"(base));
+    __hip_atomic_store(base + k, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 template <int kSc>
 __global__ __launch_bounds__(kBlock, TPT_GEN_MINWAVES) void tpt_bdpt_gen_kernel(DScene s, WfState w, int batch,
@@ -524,7 +535,11 @@ __global__ __launch_bounds__(kBlock, TPT_GEN_MINWAVES) void tpt_bdpt_gen_kernel(
         if (nm != 0) {
             const int leader = __builtin_ctzll(nm);
             unsigned base = 0;
-            if (lane_id() == leader) base = atomicAdd(q, (unsigned)__popcll(nm));
+            if (lane_id() == leader) {
+                unsigned* qa = q;  // opaque: used from SGPRs here, not held in VGPRs across the loop
+                asm volatile("" : "+s"(qa));
+                base = atomicAdd(qa, (unsigned)__popcll(nm));
+            }
             base = __shfl(base, leader);
             if (need) {
                 const int kk = k_lo + (int)base + __popcll(nm & ((1ull << lane_id()) - 1));
@@ -541,23 +556,25 @@ __global__ __launch_bounds__(kBlock, TPT_GEN_MINWAVES) void tpt_bdpt_gen_kernel(
         if (k >= 0 && !ready) {
             if (batch == 0) {
                 rs = (uint32_t)((int)wf_pixel(w, k) + 1);  // ResetRandom(i + 1), Renderer.cpp:42
-                w.acc[3 * k] = 0.0f; w.acc[3 * k + 1] = 0.0f; w.acc[3 * k + 2] = 0.0f;
+                float z = 0.0f;  // opaque: the zeros are made here, not held (spilled) across the loop
+                asm volatile("" : "+v"(z));
+                w.acc[3 * k] = z; w.acc[3 * k + 1] = z; w.acc[3 * k + 2] = z;
                 ready = true;
             } else {
                 // one gen stream: gen(f - 1) completed before this kernel started, so a
                 // plain load sees its state; two: wait for its publication
-                const unsigned long long v = w.conc ? load_rngseq(w.rngseq + k) : w.rngseq[k];
+                const unsigned long long v = w.conc ? load_rngseq(w.rngseq, k) : w.rngseq[k];
                 if ((v >> 32) == (unsigned long long)batch) {
                     rs = (uint32_t)v;
                     ready = true;
                 } else if (wait_t0 == 0) {
                     wait_t0 = (uint32_t)__builtin_amdgcn_s_memrealtime() | 1u;  // the wait starts
-                } else if (TPT_WATCHDOG && (uint32_t)__builtin_amdgcn_s_memrealtime() - wait_t0 > kStallTicks) {
+                } else if (TPT_WATCHDOG && (uint32_t)__builtin_amdgcn_s_memrealtime() - wait_t0 > w.stall_ticks) {
                     // watchdog: give up on k, publish it so later wavefronts do not wait
                     // too, and report it.  Its items keep older contents, which are
                     // always a complete sample's (ensure_wf zeroes the arrays when it
                     // allocates them), so the scan, scatter and connect stay in bounds.
-                    store_rngseq(w.rngseq + k, (unsigned long long)(batch + 1) << 32 | 1u);
+                    store_rngseq(w.rngseq, k, (unsigned long long)(batch + 1) << 32 | 1u);
                     atomicOr(w.stall, 1);
                     k = -1;
                 }
@@ -593,8 +610,13 @@ __global__ __launch_bounds__(kBlock, TPT_GEN_MINWAVES) void tpt_bdpt_gen_kernel(
                 fresh = true;  // the pixel's next sample, same stream, from the next step
             } else {
                 const unsigned long long v = (unsigned long long)(batch + 1) << 32 | rs;
-                if (w.conc) store_rngseq(w.rngseq + k, v);
-                else w.rngseq[k] = v;
+                if (TPT_DIAG_HOOKS && batch == 1 && k == w.drop_k) {
+                    // diagnostics: k's state is never published, gen(2)'s watchdog takes over
+                } else if (w.conc) {
+                    store_rngseq(w.rngseq, k, v);
+                } else {
+                    w.rngseq[k] = v;
+                }
                 k = -1;
                 ready = false;
             }
@@ -637,9 +659,11 @@ TPT_D int64_t total_tasks(const WfState& w) {
     return (int64_t)(t1 & 0xffffffffull) + (int64_t)(t1 >> 32) + (int64_t)(t2 & 0xffffffffull) + (int64_t)(t2 >> 32);
 }
 
-__global__ __launch_bounds__(kBlock) void tpt_bdpt_scatter_kernel(WfState w, unsigned* __restrict__ queue) {
+__global__ __launch_bounds__(kBlock) void tpt_bdpt_scatter_kernel(WfState w, unsigned* __restrict__ queue,
+                                                                  unsigned* __restrict__ cq) {
     const int64_t k = (int64_t)blockIdx.x * kBlock + threadIdx.x;  // item
     if (k < 8) queue[k * 16] = 0;  // gen of the next wavefront (same stream, after this kernel) starts its shards at 0
+    if (k == 8) cq[0] = 0;         // connect of this wavefront (next on the other stream) claims chunks from 0
     if (k >= w.ni) return;
     const StratRange r = strat_range(w, k);
     const int ln = r.ln, cn = w.cnt[k] & 0xffff;
@@ -654,10 +678,84 @@ __global__ __launch_bounds__(kBlock) void tpt_bdpt_scatter_kernel(WfState w, uns
     }
 }
 
-// One lane per strategy, grid-stride in wave-sized steps so that every lane of a
-// wave stays in the loop until the wave is done (splat_wave needs the whole wave).
+// One strategy (task g) of connect: PathWeight, the result at its task index (t > 1)
+// or the splat of the wave (t = 1; call with every lane of the wave).
+TPT_D void conn_task(const DScene& s, const WfState& w, float* __restrict__ splat, int64_t g, bool on, V3 eye) {
+    V3 v = v3s(0.0f), lx = eye;
+    bool sp = false;
+    if (on) {
+        const unsigned tk = w.task[g];
+        const int64_t k = (int64_t)(tk & kTaskPixelMask);
+        const int t = (int)((tk >> 22) & 31), sl = (int)(tk >> 27);
+        GlobPaths P;
+        P.rec = rec_at(w.rec, k, 0);
+        v = vmax0(path_weight(s, P, sl, t));
+        if (t > 1) {  // the result stays in task order; fold finds it from (t, s)
+            w.res[3 * g] = v.x;
+            w.res[3 * g + 1] = v.y;
+            w.res[3 * g + 2] = v.z;
+        } else if (splat) {
+            sp = true;
+            lx = P.lit(sl - 1).x;
+        }
+    }
+    // t = 1: DrawToImage of the light vertex (BDPT.cpp:303-305), whole wave
+    if (splat) splat_wave(s, sp, lx, eye, v, splat);
+}
+
+// Coherent connection order (round 4).  The shadow query of a strategy
+// (BDPT.cpp:205) from the camera-side vertex toward the light-side one walks the
+// bunny's tree when the ray passes the walk group's box; dealt pixel-major, the 64
+// lanes of a wave walk 64 unrelated parts of the mesh (per-lane incoherent node
+// fetches: the kernel waits on memory for 44 % of its wave time).  So each wave takes
+// a chunk of kSortN consecutive tasks (a work queue: chunks are claimed with one
+// atomic), sorts them in LDS by a key -- class, whether the ray passes the walk
+// group's box, then the ray's direction octant and the Morton cell of its entry point
+// into that box -- and runs them in that order.  Every task still writes its result
+// at its own task index (fold is unchanged) and splats are fp32 atomics in any
+// order, so results are unchanged; the key only decides which lanes run together.
+#ifndef TPT_CONN_SORT
+#define TPT_CONN_SORT 1  // 1: scenes with walk groups, 2: every scene, 0: off
+#endif
+#ifndef TPT_CONN_SORT_R
+#define TPT_CONN_SORT_R 8  // tasks per lane per sorted chunk (kSortN = 64 R, <= 1024)
+#endif
+constexpr int kSortN = 64 * TPT_CONN_SORT_R;
+static_assert((kSortN & (kSortN - 1)) == 0 && kSortN <= 1024, "a power of two, local index in 10 bits");
+TPT_D unsigned spread3(unsigned v) {  // 4 bits -> every third bit
+    return (v & 1u) | (v & 2u) << 2 | (v & 4u) << 4 | (v & 8u) << 6;
+}
+// 18-bit key: class (2) | walk (1) | octant (3) | Morton cell of the box entry (12)
+TPT_D unsigned conn_key(const DScene& s, const WfState& w, int64_t g, int gi) {
+    const unsigned tk = w.task[g];
+    const int t = (int)((tk >> 22) & 31), sl = (int)(tk >> 27);
+    const unsigned cls = sl == 0 ? 0u : t == 1 ? 3u : sl == 1 ? 2u : 1u;
+    if (cls == 0 || gi < 0) return cls << 16;
+    const DNode gn = s.groups[gi];
+    const float bx[6] = {gn.bmin[0], gn.bmin[1], gn.bmin[2], gn.bmax[0], gn.bmax[1], gn.bmax[2]};
+    const float4* r = rec_at(w.rec, (int64_t)(tk & kTaskPixelMask), 0);
+    const float4 a = r[(t - 1) * kRecV], b = r[(kMaxLen + sl - 1) * kRecV];
+    const float dx = b.x - a.x, dy = b.y - a.y, dz = b.z - a.z;
+    const float ix = __builtin_amdgcn_rcpf(dx), iy = __builtin_amdgcn_rcpf(dy), iz = __builtin_amdgcn_rcpf(dz);
+    const float ax = (bx[0] - a.x) * ix, cx = (bx[3] - a.x) * ix;
+    const float ay = (bx[1] - a.y) * iy, cy = (bx[4] - a.y) * iy;
+    const float az = (bx[2] - a.z) * iz, cz = (bx[5] - a.z) * iz;
+    const float t0 = fmaxf(fmaxf(0.0f, fminf(ax, cx)), fmaxf(fminf(ay, cy), fminf(az, cz)));
+    const float t1 = fminf(fmaxf(ax, cx), fminf(fmaxf(ay, cy), fmaxf(az, cz)));
+    if (!(t0 <= t1)) return cls << 16;  // misses the box (NaN: either way, only a heuristic)
+    auto cell = [](float p, float lo, float hi) {
+        const float u = (p - lo) * 16.0f / (hi - lo);
+        return u >= 15.0f ? 15u : u > 0.0f ? (unsigned)u : 0u;
+    };
+    const unsigned m = spread3(cell(a.x + t0 * dx, bx[0], bx[3])) | spread3(cell(a.y + t0 * dy, bx[1], bx[4])) << 1 |
+                       spread3(cell(a.z + t0 * dz, bx[2], bx[5])) << 2;
+    const unsigned oct = (dx < 0.0f ? 1u : 0u) | (dy < 0.0f ? 2u : 0u) | (dz < 0.0f ? 4u : 0u);
+    return cls << 16 | 1u << 15 | oct << 12 | m;
+}
+
 template <int kSc>
-__global__ __launch_bounds__(kBlock, TPT_CONN_MINWAVES) void tpt_bdpt_conn_kernel(DScene s, WfState w, float* __restrict__ splat) {
+__global__ __launch_bounds__(kBlock, TPT_CONN_MINWAVES) void tpt_bdpt_conn_kernel(DScene s, WfState w, float* __restrict__ splat,
+                                                                                  unsigned* __restrict__ cq) {
     stage_scene<kSc>(s);
     __shared__ QScratch qsm[kBlock / 64];
     s.qs = qsm;
@@ -668,30 +766,57 @@ __global__ __launch_bounds__(kBlock, TPT_CONN_MINWAVES) void tpt_bdpt_conn_kerne
     }
     const int64_t total = total_tasks(w);
     const V3 eye = v3(s.eye[0], s.eye[1], s.eye[2]);
-    for (int64_t g0 = (int64_t)blockIdx.x * kBlock + (threadIdx.x & ~63); g0 < total;
-         g0 += (int64_t)gridDim.x * kBlock) {
-        const int64_t g = g0 + lane_id();
-        V3 v = v3s(0.0f), lx = eye;
-        bool sp = false;
-        if (g < total) {
-            const unsigned tk = w.task[g];
-            const int64_t k = (int64_t)(tk & kTaskPixelMask);
-            const int t = (int)((tk >> 22) & 31), sl = (int)(tk >> 27);
-            GlobPaths P;
-            P.rec = rec_at(w.rec, k, 0);
-            v = vmax0(path_weight(s, P, sl, t));
-            if (t > 1) {  // the result stays in task order; fold finds it from (t, s)
-                const int64_t gr = g;
-                w.res[3 * gr] = v.x;
-                w.res[3 * gr + 1] = v.y;
-                w.res[3 * gr + 2] = v.z;
-            } else if (splat) {
-                sp = true;
-                lx = P.lit(sl - 1).x;
-            }
+    constexpr bool kSort = TPT_CONN_SORT == 2 || (TPT_CONN_SORT == 1 && kSc == 2);
+    if constexpr (!kSort) {
+        // grid-stride in wave-sized steps: every lane of a wave stays in the loop until
+        // the wave is done (splat_wave needs the whole wave)
+        for (int64_t g0 = (int64_t)blockIdx.x * kBlock + (threadIdx.x & ~63); g0 < total;
+             g0 += (int64_t)gridDim.x * kBlock) {
+            const int64_t g = g0 + lane_id();
+            conn_task(s, w, splat, g, g < total, eye);
         }
-        // t = 1: DrawToImage of the light vertex (BDPT.cpp:303-305), whole wave
-        if (splat) splat_wave(s, sp, lx, eye, v, splat);
+    } else {
+        __shared__ unsigned srt_all[kBlock / 64][kSortN];
+        // wave index in an SGPR and the lane from mbcnt at each use: nothing per-lane is
+        // held (spilled) across the connections
+        unsigned* srt = srt_all[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)];
+        int box = -1;  // the first walk group (its box keys the sort)
+        for (int gi = s.ngroup - 1; gi >= 0; --gi)
+            if (s.groups[gi].b < 0) box = gi;
+        for (;;) {
+            unsigned ch = 0;
+            if (lane_id() == 0) {
+                unsigned* q = cq;
+                asm volatile("" : "+s"(q));
+                ch = atomicAdd(q, 1u);
+            }
+            const int64_t c0 = (int64_t)__builtin_amdgcn_readfirstlane(__shfl(ch, 0)) * kSortN;
+            if (c0 >= total) break;
+            for (int j = lane_id(); j < kSortN; j += 64) {
+                const int64_t g = c0 + j;
+                const unsigned key = g < total ? conn_key(s, w, g, box) : 0x3ffffu;
+                srt[j] = key << 10 | (unsigned)j;
+            }
+            wave_lds_sync();
+            for (int kk = 2; kk <= kSortN; kk <<= 1) {  // bitonic sort of the wave's chunk
+                for (int jj = kk >> 1; jj > 0; jj >>= 1) {
+                    for (int p = lane_id(); p < kSortN / 2; p += 64) {
+                        const int i = (p & ~(jj - 1)) << 1 | (p & (jj - 1)), l = i + jj;
+                        const unsigned x = srt[i], y = srt[l];
+                        if ((x > y) == ((i & kk) == 0)) {
+                            srt[i] = y;
+                            srt[l] = x;
+                        }
+                    }
+                    wave_lds_sync();
+                }
+            }
+            for (int j0 = 0; j0 < kSortN; j0 += 64) {
+                const int64_t g = c0 + (int64_t)(srt[j0 + lane_id()] & 1023u);
+                conn_task(s, w, splat, g, g < total, eye);
+            }
+            wave_lds_sync();  // the next chunk reuses srt
+        }
     }
 }
 
@@ -813,6 +938,8 @@ __global__ __launch_bounds__(kBlock) void tpt_intersect_kernel(DScene s, const f
 // 0.898; whole frames unchanged (bunny 256 spp 1112 / 1089 / 1091 ms)
 #endif
 constexpr int kWfBufs = TPT_WF_BUFS;
+// per wavefront buffer: gen's 8 shard counters (64 B apart), then connect's chunk counters
+constexpr size_t kQueueBytes = kWfBufs * 8 * 64 + kWfBufs * 64;
 static_assert(kWfBufs >= 2 && kWfBufs <= 4, "2 to 4 wavefront buffers");
 
 struct tpt_ctx {
@@ -842,6 +969,8 @@ struct tpt_ctx {
     hipStream_t stream2 = nullptr;    // connect + fold
     hipStream_t stream3 = nullptr;    // gen / scan / scatter of the odd wavefronts (even ones: stream)
     hipEvent_t ev_gen[kWfBufs]{}, ev_fold[kWfBufs]{}, ev_start = nullptr;
+    unsigned stall_ticks = kStallTicks;  // gen watchdog limit (TPT_DIAG_HOOKS builds: per render from the env)
+    int drop_k = -1;                     // TPT_DIAG_HOOKS builds only (see there)
     void* scan_tmp = nullptr;         // two scratch areas: the gen streams scan concurrently
     void* scan_tmp_g[2]{};            // per gen stream
     size_t scan_bytes = 0;
@@ -1011,7 +1140,7 @@ int launch_bdpt_chunk(tpt_ctx* c, int spp, int64_t begin, int64_t stride, int64_
     // both gen streams start after everything queued so far; the pixel states and the
     // queue counters of both buffers start at 0
     HIP_TRY(c, hipMemsetAsync(c->wf[0].rngseq, 0, count * sizeof(unsigned long long), c->stream));
-    HIP_TRY(c, hipMemsetAsync(c->queue, 0, kWfBufs * 8 * 64, c->stream));
+    HIP_TRY(c, hipMemsetAsync(c->queue, 0, kQueueBytes, c->stream));
     HIP_TRY(c, hipEventRecord(c->ev_start, c->stream));
     HIP_TRY(c, hipStreamWaitEvent(s2, c->ev_start, 0));
     if (gs[1] != gs[0]) HIP_TRY(c, hipStreamWaitEvent(gs[1], c->ev_start, 0));
@@ -1033,6 +1162,15 @@ int launch_bdpt_chunk(tpt_ctx* c, int spp, int64_t begin, int64_t stride, int64_
     int64_t gb = (int64_t)std::max(per_cu, 1) * std::max(c->num_cu, 1) * gen_q / 32;
     gb = std::min<int64_t>(gb, ((int64_t)pblocks + 7) / 8 * 8);
     const unsigned gblocks = (unsigned)std::max<int64_t>(8, gb / 8 * 8);
+    // The two-stream hand-off (gen(f) waits, lane by lane, on gen(f - 1)'s publications)
+    // cannot deadlock only while gen(f - 1) can always be scheduled: gen(f) spins on at
+    // most its own grid, so each gen grid must leave at least half of the chip's
+    // resident workgroups to the other kernels.  (connect never waits; it frees its
+    // slots as it finishes.)
+    const int64_t resident = (int64_t)std::max(per_cu, 1) * std::max(c->num_cu, 1);
+    if (two_gen && 2 * (int64_t)gblocks > resident)
+        return fail(c, TPT_E_DEVICE, "BDPT: gen grid of " + std::to_string(gblocks) + " workgroups exceeds half of the " +
+                                         std::to_string(resident) + " resident ones (two-stream hand-off invariant)");
     const float inv = 1.0f / spp;
     for (int f = 0, it0 = 0; it0 < spp; ++f, it0 += nb) {
         const int b = f % kWfBufs, gsi = f & 1;  // wavefront buffer, gen stream
@@ -1045,9 +1183,12 @@ int launch_bdpt_chunk(tpt_ctx* c, int spp, int64_t begin, int64_t stride, int64_
         w.ni = (int64_t)w.nb * count;
         w.bounces = c->counters;
         w.stall = reinterpret_cast<int*>(c->counters + 4);
+        w.stall_ticks = c->stall_ticks;
+        w.drop_k = c->drop_k;
         w.conc = two_gen ? 1 : 0;
         w.nbuf = kWfBufs;
         unsigned* queue = c->queue + b * 8 * 16;
+        unsigned* cq = c->queue + kWfBufs * 8 * 16 + b * 16;  // connect's chunk counter (sorted connect)
         const unsigned iblocks = (unsigned)((w.ni + kBlock - 1) / kBlock);
         const unsigned cblocks = (unsigned)std::min<int64_t>(c->sc == 2 ? TPT_CONN_GRID_WALK : TPT_CONN_GRID,
                                                              (w.ni * 24 + kBlock - 1) / kBlock + 1);
@@ -1059,10 +1200,10 @@ int launch_bdpt_chunk(tpt_ctx* c, int spp, int64_t begin, int64_t stride, int64_
         bytes = c->scan_bytes;
         HIP_TRY(c, rocprim::inclusive_scan(c->scan_tmp_g[gsi], bytes, w.np2, w.incl2, (size_t)w.ni,
                                            rocprim::plus<unsigned long long>(), gs[gsi]));
-        hipLaunchKernelGGL(tpt_bdpt_scatter_kernel, dim3(iblocks), dim3(kBlock), 0, gs[gsi], w, queue);
+        hipLaunchKernelGGL(tpt_bdpt_scatter_kernel, dim3(iblocks), dim3(kBlock), 0, gs[gsi], w, queue, cq);
         HIP_TRY(c, hipEventRecord(c->ev_gen[b], gs[gsi]));
         HIP_TRY(c, hipStreamWaitEvent(s2, c->ev_gen[b], 0));
-        hipLaunchKernelGGL(conn_k, dim3(cblocks), dim3(kBlock), shmem, s2, c->ds, w, dsplat);
+        hipLaunchKernelGGL(conn_k, dim3(cblocks), dim3(kBlock), shmem, s2, c->ds, w, dsplat, cq);
         if (w.nb == 1) {
             hipLaunchKernelGGL(tpt_bdpt_fold_kernel, dim3(pblocks), dim3(kBlock), 0, s2, w, inv);
         } else {
@@ -1126,6 +1267,12 @@ int launch(tpt_ctx* c, int mode, int flags, int spp, int64_t begin, int64_t stri
         hipLaunchKernelGGL(k, dim3((unsigned)((lanes + kBlock - 1) / kBlock)), dim3(kBlock), shmem, c->stream, c->ds,
                            spp, begin, stride, count, dlist, drows, c->counters);
     } else {
+#if TPT_DIAG_HOOKS
+        const char* dk = std::getenv("TPT_DIAG_DROP_PUBLISH");
+        const char* dt = std::getenv("TPT_DIAG_STALL_TICKS");
+        c->drop_k = dk && *dk ? std::atoi(dk) : -1;
+        c->stall_ticks = dt && *dt ? (unsigned)std::strtoul(dt, nullptr, 10) : kStallTicks;
+#endif
         // Shards larger than kWfChunk pixel streams run as consecutive chunks.
         const int64_t chunk = std::min(count, kWfChunk), last = count - (count - 1) / kWfChunk * kWfChunk;
         int rc = ensure_wf(c, std::max(chunk * wf_iters(chunk, spp), last * wf_iters(last, spp)));
@@ -1220,7 +1367,7 @@ int tpt_create(int device, tpt_ctx** out) {
         hipStreamCreateWithFlags(&c->stream3, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_start, hipEventDisableTiming) != hipSuccess ||
         hipMalloc(&c->counters, sizeof(unsigned long long) * 32) != hipSuccess ||
-        hipMalloc(&c->queue, kWfBufs * 8 * 64) != hipSuccess ||
+        hipMalloc(&c->queue, kQueueBytes) != hipSuccess ||
         hipDeviceGetAttribute(&c->num_cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) {
         tpt_destroy(c);  // releases what was created
         return TPT_E_DEVICE;

@@ -480,7 +480,9 @@ struct QScratch {         // per wave, in LDS
     int32_t prim[kQC];
     uint32_t flag[64];    // shadow query: the owner's ray is blocked
 };
-TPT_D QScratch* wave_qs(const DScene& s) { return reinterpret_cast<QScratch*>(s.qs) + (threadIdx.x >> 6); }
+TPT_D QScratch* wave_qs(const DScene& s) {  // wave index in an SGPR: no per-lane copy of the base is held
+    return reinterpret_cast<QScratch*>(s.qs) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+}
 // LDS writes of some lanes made visible to reads of other lanes of the same wave
 TPT_D void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
