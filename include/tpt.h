@@ -129,6 +129,11 @@ typedef struct tpt_render_params {
     int32_t reserved;
 } tpt_render_params;
 
+/* tpt_stats grew in ABI 2 (nonfinite, nonfinite_splat: 56 bytes, was 40), and every
+ * render entry writes the whole struct.  A caller must check
+ * tpt_abi_version() == TPT_ABI_VERSION before its first render call (a binary built
+ * against ABI 1 would be overwritten past its 40-byte stats object); the in-reference
+ * binding and pytpt do. */
 typedef struct tpt_stats {
     int64_t pixels;               /* pixels rendered by this call */
     int64_t samples;              /* pixels * spp */

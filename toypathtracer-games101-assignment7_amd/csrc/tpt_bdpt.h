@@ -210,7 +210,10 @@ TPT_D V3 path_weight(const DScene& s, const P& paths, int sl, int tl) {
         // skip zeros, so returning +0 without the test is exact.
         const V3 c = vmax0(res);
         if (c.x == 0.0f && c.y == 0.0f && c.z == 0.0f) return v3s(0.0f);
-        if (shadow_v(s, cz, ly)) return v3s(0.0f);
+#ifndef TPT_DIAG_NO_CONN_SHADOW
+#define TPT_DIAG_NO_CONN_SHADOW 0  // diagnostics builds only (timing attribution; wrong images)
+#endif
+        if (!TPT_DIAG_NO_CONN_SHADOW && shadow_v(s, cz, ly)) return v3s(0.0f);
     }
     return res;
 }

@@ -659,11 +659,9 @@ TPT_D int64_t total_tasks(const WfState& w) {
     return (int64_t)(t1 & 0xffffffffull) + (int64_t)(t1 >> 32) + (int64_t)(t2 & 0xffffffffull) + (int64_t)(t2 >> 32);
 }
 
-__global__ __launch_bounds__(kBlock) void tpt_bdpt_scatter_kernel(WfState w, unsigned* __restrict__ queue,
-                                                                  unsigned* __restrict__ cq) {
+__global__ __launch_bounds__(kBlock) void tpt_bdpt_scatter_kernel(WfState w, unsigned* __restrict__ queue) {
     const int64_t k = (int64_t)blockIdx.x * kBlock + threadIdx.x;  // item
     if (k < 8) queue[k * 16] = 0;  // gen of the next wavefront (same stream, after this kernel) starts its shards at 0
-    if (k == 8) cq[0] = 0;         // connect of this wavefront (next on the other stream) claims chunks from 0
     if (k >= w.ni) return;
     const StratRange r = strat_range(w, k);
     const int ln = r.ln, cn = w.cnt[k] & 0xffff;
@@ -703,59 +701,49 @@ TPT_D void conn_task(const DScene& s, const WfState& w, float* __restrict__ spla
     if (splat) splat_wave(s, sp, lx, eye, v, splat);
 }
 
-// Coherent connection order (round 4).  The shadow query of a strategy
-// (BDPT.cpp:205) from the camera-side vertex toward the light-side one walks the
-// bunny's tree when the ray passes the walk group's box; dealt pixel-major, the 64
-// lanes of a wave walk 64 unrelated parts of the mesh (per-lane incoherent node
-// fetches: the kernel waits on memory for 44 % of its wave time).  So each wave takes
-// a chunk of kSortN consecutive tasks (a work queue: chunks are claimed with one
-// atomic), sorts them in LDS by a key -- class, whether the ray passes the walk
-// group's box, then the ray's direction octant and the Morton cell of its entry point
-// into that box -- and runs them in that order.  Every task still writes its result
-// at its own task index (fold is unchanged) and splats are fp32 atomics in any
-// order, so results are unchanged; the key only decides which lanes run together.
+// Walker partition (round 4).  For a scene with walk groups the shadow query of a
+// strategy (BDPT.cpp:205), from the camera-side vertex toward the light-side one,
+// walks the mesh's tree when its ray passes the walk group's box; dealt pixel-major,
+// a wave of 64 strategies almost always holds a few such lanes, and the whole wave
+// waits on their walks.  So each wave takes kSortN = 64 R consecutive tasks, marks
+// the ones whose ray passes the box (a cheap approximate slab test: the mark only
+// decides which lanes run together), and runs them in R rounds with the unmarked
+// tasks first and the marked ones last, each group in task order (a stable
+// partition through ballots; the permutation sits in LDS).  Every task still writes
+// its result at its own task index (fold is unchanged) and splats are fp32 atomics
+// in any order, so results are unchanged.
 #ifndef TPT_CONN_SORT
 #define TPT_CONN_SORT 1  // 1: scenes with walk groups, 2: every scene, 0: off
 #endif
 #ifndef TPT_CONN_SORT_R
-#define TPT_CONN_SORT_R 8  // tasks per lane per sorted chunk (kSortN = 64 R, <= 1024)
+#define TPT_CONN_SORT_R 4  // rounds of 64 tasks per partitioned chunk
 #endif
-constexpr int kSortN = 64 * TPT_CONN_SORT_R;
-static_assert((kSortN & (kSortN - 1)) == 0 && kSortN <= 1024, "a power of two, local index in 10 bits");
-TPT_D unsigned spread3(unsigned v) {  // 4 bits -> every third bit
-    return (v & 1u) | (v & 2u) << 2 | (v & 4u) << 4 | (v & 8u) << 6;
-}
-// 18-bit key: class (2) | walk (1) | octant (3) | Morton cell of the box entry (12)
-TPT_D unsigned conn_key(const DScene& s, const WfState& w, int64_t g, int gi) {
+constexpr int kSortR = TPT_CONN_SORT_R;
+constexpr int kSortN = 64 * kSortR;
+static_assert(kSortR >= 1 && kSortR <= 16, "chunk of 64 R tasks");
+// Does task g's shadow ray (camera-side vertex toward the light-side one) pass the box
+// of walk group gi?  False for s = 0 (no shadow query).
+TPT_D bool conn_marked(const DScene& s, const WfState& w, int64_t g, int gi) {
     const unsigned tk = w.task[g];
     const int t = (int)((tk >> 22) & 31), sl = (int)(tk >> 27);
-    const unsigned cls = sl == 0 ? 0u : t == 1 ? 3u : sl == 1 ? 2u : 1u;
-    if (cls == 0 || gi < 0) return cls << 16;
+    if (sl == 0) return false;
     const DNode gn = s.groups[gi];
-    const float bx[6] = {gn.bmin[0], gn.bmin[1], gn.bmin[2], gn.bmax[0], gn.bmax[1], gn.bmax[2]};
     const float4* r = rec_at(w.rec, (int64_t)(tk & kTaskPixelMask), 0);
     const float4 a = r[(t - 1) * kRecV], b = r[(kMaxLen + sl - 1) * kRecV];
-    const float dx = b.x - a.x, dy = b.y - a.y, dz = b.z - a.z;
-    const float ix = __builtin_amdgcn_rcpf(dx), iy = __builtin_amdgcn_rcpf(dy), iz = __builtin_amdgcn_rcpf(dz);
-    const float ax = (bx[0] - a.x) * ix, cx = (bx[3] - a.x) * ix;
-    const float ay = (bx[1] - a.y) * iy, cy = (bx[4] - a.y) * iy;
-    const float az = (bx[2] - a.z) * iz, cz = (bx[5] - a.z) * iz;
+    const float ix = __builtin_amdgcn_rcpf(b.x - a.x), iy = __builtin_amdgcn_rcpf(b.y - a.y),
+                iz = __builtin_amdgcn_rcpf(b.z - a.z);
+    const float ax = (gn.bmin[0] - a.x) * ix, cx = (gn.bmax[0] - a.x) * ix;
+    const float ay = (gn.bmin[1] - a.y) * iy, cy = (gn.bmax[1] - a.y) * iy;
+    const float az = (gn.bmin[2] - a.z) * iz, cz = (gn.bmax[2] - a.z) * iz;
     const float t0 = fmaxf(fmaxf(0.0f, fminf(ax, cx)), fmaxf(fminf(ay, cy), fminf(az, cz)));
     const float t1 = fminf(fmaxf(ax, cx), fminf(fmaxf(ay, cy), fmaxf(az, cz)));
-    if (!(t0 <= t1)) return cls << 16;  // misses the box (NaN: either way, only a heuristic)
-    auto cell = [](float p, float lo, float hi) {
-        const float u = (p - lo) * 16.0f / (hi - lo);
-        return u >= 15.0f ? 15u : u > 0.0f ? (unsigned)u : 0u;
-    };
-    const unsigned m = spread3(cell(a.x + t0 * dx, bx[0], bx[3])) | spread3(cell(a.y + t0 * dy, bx[1], bx[4])) << 1 |
-                       spread3(cell(a.z + t0 * dz, bx[2], bx[5])) << 2;
-    const unsigned oct = (dx < 0.0f ? 1u : 0u) | (dy < 0.0f ? 2u : 0u) | (dz < 0.0f ? 4u : 0u);
-    return cls << 16 | 1u << 15 | oct << 12 | m;
+    return t0 <= t1;
 }
 
+// One lane per strategy, grid-stride in wave-sized steps so that every lane of a
+// wave stays in the loop until the wave is done (splat_wave needs the whole wave).
 template <int kSc>
-__global__ __launch_bounds__(kBlock, TPT_CONN_MINWAVES) void tpt_bdpt_conn_kernel(DScene s, WfState w, float* __restrict__ splat,
-                                                                                  unsigned* __restrict__ cq) {
+__global__ __launch_bounds__(kBlock, TPT_CONN_MINWAVES) void tpt_bdpt_conn_kernel(DScene s, WfState w, float* __restrict__ splat) {
     stage_scene<kSc>(s);
     __shared__ QScratch qsm[kBlock / 64];
     s.qs = qsm;
@@ -766,53 +754,42 @@ __global__ __launch_bounds__(kBlock, TPT_CONN_MINWAVES) void tpt_bdpt_conn_kerne
     }
     const int64_t total = total_tasks(w);
     const V3 eye = v3(s.eye[0], s.eye[1], s.eye[2]);
-    constexpr bool kSort = TPT_CONN_SORT == 2 || (TPT_CONN_SORT == 1 && kSc == 2);
-    if constexpr (!kSort) {
-        // grid-stride in wave-sized steps: every lane of a wave stays in the loop until
-        // the wave is done (splat_wave needs the whole wave)
+    constexpr bool kPart = TPT_CONN_SORT == 2 || (TPT_CONN_SORT == 1 && kSc == 2);
+    if constexpr (!kPart) {
         for (int64_t g0 = (int64_t)blockIdx.x * kBlock + (threadIdx.x & ~63); g0 < total;
              g0 += (int64_t)gridDim.x * kBlock) {
             const int64_t g = g0 + lane_id();
             conn_task(s, w, splat, g, g < total, eye);
         }
     } else {
-        __shared__ unsigned srt_all[kBlock / 64][kSortN];
-        // wave index in an SGPR and the lane from mbcnt at each use: nothing per-lane is
-        // held (spilled) across the connections
-        unsigned* srt = srt_all[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)];
-        int box = -1;  // the first walk group (its box keys the sort)
+        __shared__ uint16_t srt_all[kBlock / 64][kSortN];
+        const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+        uint16_t* srt = srt_all[wv];
+        int box = -1;  // the first walk group
         for (int gi = s.ngroup - 1; gi >= 0; --gi)
             if (s.groups[gi].b < 0) box = gi;
-        for (;;) {
-            unsigned ch = 0;
-            if (lane_id() == 0) {
-                unsigned* q = cq;
-                asm volatile("" : "+s"(q));
-                ch = atomicAdd(q, 1u);
+        for (int64_t c0 = ((int64_t)blockIdx.x * (kBlock / 64) + wv) * kSortN; c0 < total;
+             c0 += (int64_t)gridDim.x * kBlock * kSortR) {
+            unsigned mk = 0;  // bit r: the lane's task of round r is marked
+            int nu = 0;       // unmarked tasks of the chunk (wave-uniform)
+            for (int r = 0; r < kSortR; ++r) {
+                const int64_t g = c0 + r * 64 + lane_id();
+                const bool m = box >= 0 && g < total && conn_marked(s, w, g, box);
+                mk |= (m ? 1u : 0u) << r;
+                nu += 64 - __popcll(__ballot(m));
             }
-            const int64_t c0 = (int64_t)__builtin_amdgcn_readfirstlane(__shfl(ch, 0)) * kSortN;
-            if (c0 >= total) break;
-            for (int j = lane_id(); j < kSortN; j += 64) {
-                const int64_t g = c0 + j;
-                const unsigned key = g < total ? conn_key(s, w, g, box) : 0x3ffffu;
-                srt[j] = key << 10 | (unsigned)j;
+            int pu = 0, pm = nu;  // next slot of each group
+            for (int r = 0; r < kSortR; ++r) {
+                const bool m = (mk >> r) & 1u;
+                const uint64_t bm = __ballot(m);
+                const int before = mbcnt64(m ? bm : ~bm);
+                srt[(m ? pm : pu) + before] = (uint16_t)(r * 64 + lane_id());
+                pm += __popcll(bm);
+                pu += 64 - __popcll(bm);
             }
             wave_lds_sync();
-            for (int kk = 2; kk <= kSortN; kk <<= 1) {  // bitonic sort of the wave's chunk
-                for (int jj = kk >> 1; jj > 0; jj >>= 1) {
-                    for (int p = lane_id(); p < kSortN / 2; p += 64) {
-                        const int i = (p & ~(jj - 1)) << 1 | (p & (jj - 1)), l = i + jj;
-                        const unsigned x = srt[i], y = srt[l];
-                        if ((x > y) == ((i & kk) == 0)) {
-                            srt[i] = y;
-                            srt[l] = x;
-                        }
-                    }
-                    wave_lds_sync();
-                }
-            }
             for (int j0 = 0; j0 < kSortN; j0 += 64) {
-                const int64_t g = c0 + (int64_t)(srt[j0 + lane_id()] & 1023u);
+                const int64_t g = c0 + (int64_t)srt[j0 + lane_id()];
                 conn_task(s, w, splat, g, g < total, eye);
             }
             wave_lds_sync();  // the next chunk reuses srt
@@ -938,8 +915,8 @@ __global__ __launch_bounds__(kBlock) void tpt_intersect_kernel(DScene s, const f
 // 0.898; whole frames unchanged (bunny 256 spp 1112 / 1089 / 1091 ms)
 #endif
 constexpr int kWfBufs = TPT_WF_BUFS;
-// per wavefront buffer: gen's 8 shard counters (64 B apart), then connect's chunk counters
-constexpr size_t kQueueBytes = kWfBufs * 8 * 64 + kWfBufs * 64;
+// per wavefront buffer: gen's 8 shard counters, 64 B apart
+constexpr size_t kQueueBytes = kWfBufs * 8 * 64;
 static_assert(kWfBufs >= 2 && kWfBufs <= 4, "2 to 4 wavefront buffers");
 
 struct tpt_ctx {
@@ -1103,6 +1080,17 @@ int64_t shard_count(int64_t npix, int64_t begin, int64_t stride) {
 // 932.6 ms.
 #define TPT_GEN_GRID_Q 10
 #endif
+#ifndef TPT_GEN_GRID_Q_WALK
+// ... for scenes with walk groups (the bunny), whose connect runs the walker partition:
+// connect got 21 % cheaper (serialised kernel trace, bunny BDPT 64 spp: 4.55 -> 3.60 ms
+// per wavefront), so gen, which now bounds the frame, takes a larger share.  Same-box
+// sweep, bunny BDPT 256 spp with the partition: 10 -> 925, 11 -> 866, 12 -> 799,
+// 13 -> 798, 14 -> 813 ms (no partition, 10: 917 ms).
+#define TPT_GEN_GRID_Q_WALK 12
+#endif
+#ifndef TPT_GEN_GRID_Q_WALK2
+#define TPT_GEN_GRID_Q_WALK2 12  // ... when two gen kernels run at once (shards: wavefronts of >= 3 iterations)
+#endif
 #ifndef TPT_GEN2_MIN_NB
 #define TPT_GEN2_MIN_NB 3  // two gen streams when a wavefront holds >= this many iterations (whole frames,
                            // 2 iterations: one stream, bunny BDPT 256 spp 931.7 -> 919.2 ms, Standard 440.8 either way)
@@ -1128,7 +1116,7 @@ int launch_bdpt_chunk(tpt_ctx* c, int spp, int64_t begin, int64_t stride, int64_
     // s2.  The wavefront state is double-buffered: buffer f & 1 is rewritten by
     // gen(f + 2) only after fold(f).  Per pixel the order is kept: gen(f) samples after
     // gen(f - 1) (rngseq), fold is sequential on s2 (acc, splat).
-    const int nb = wf_iters(count, spp);
+    const int nb = (int)std::min<int64_t>(wf_iters(count, spp), std::max<int64_t>(1, c->wf_cap / count));
     hipStream_t s2 = TPT_BDPT_SERIAL ? c->stream : c->stream2;
     // The second gen stream only where wavefronts hold several iterations (small
     // shards: a lane runs nb samples of one pixel, so gen's tail is long).  For a
@@ -1151,7 +1139,7 @@ int launch_bdpt_chunk(tpt_ctx* c, int spp, int64_t begin, int64_t stride, int64_
 #ifndef TPT_CONN_GRID_WALK
 #define TPT_CONN_GRID_WALK 8192  // ... and scenes with walk groups (bunny BDPT 256 spp: 8192 / 16384 -> 928 / 935 ms)
 #endif
-    const int gen_q = TPT_GEN_GRID_Q;
+    const int gen_q = c->sc == 2 ? (two_gen ? TPT_GEN_GRID_Q_WALK2 : TPT_GEN_GRID_Q_WALK) : TPT_GEN_GRID_Q;
     // persistent gen grid: as many workgroups as are resident at once, a multiple of
     // the 8 queue shards, and no more than the pixels need
     const auto gen_k = c->sc == 2 ? tpt_bdpt_gen_kernel<2> : c->sc == 1 ? tpt_bdpt_gen_kernel<1> : tpt_bdpt_gen_kernel<0>;
@@ -1188,7 +1176,6 @@ int launch_bdpt_chunk(tpt_ctx* c, int spp, int64_t begin, int64_t stride, int64_
         w.conc = two_gen ? 1 : 0;
         w.nbuf = kWfBufs;
         unsigned* queue = c->queue + b * 8 * 16;
-        unsigned* cq = c->queue + kWfBufs * 8 * 16 + b * 16;  // connect's chunk counter (sorted connect)
         const unsigned iblocks = (unsigned)((w.ni + kBlock - 1) / kBlock);
         const unsigned cblocks = (unsigned)std::min<int64_t>(c->sc == 2 ? TPT_CONN_GRID_WALK : TPT_CONN_GRID,
                                                              (w.ni * 24 + kBlock - 1) / kBlock + 1);
@@ -1200,10 +1187,10 @@ int launch_bdpt_chunk(tpt_ctx* c, int spp, int64_t begin, int64_t stride, int64_
         bytes = c->scan_bytes;
         HIP_TRY(c, rocprim::inclusive_scan(c->scan_tmp_g[gsi], bytes, w.np2, w.incl2, (size_t)w.ni,
                                            rocprim::plus<unsigned long long>(), gs[gsi]));
-        hipLaunchKernelGGL(tpt_bdpt_scatter_kernel, dim3(iblocks), dim3(kBlock), 0, gs[gsi], w, queue, cq);
+        hipLaunchKernelGGL(tpt_bdpt_scatter_kernel, dim3(iblocks), dim3(kBlock), 0, gs[gsi], w, queue);
         HIP_TRY(c, hipEventRecord(c->ev_gen[b], gs[gsi]));
         HIP_TRY(c, hipStreamWaitEvent(s2, c->ev_gen[b], 0));
-        hipLaunchKernelGGL(conn_k, dim3(cblocks), dim3(kBlock), shmem, s2, c->ds, w, dsplat, cq);
+        hipLaunchKernelGGL(conn_k, dim3(cblocks), dim3(kBlock), shmem, s2, c->ds, w, dsplat);
         if (w.nb == 1) {
             hipLaunchKernelGGL(tpt_bdpt_fold_kernel, dim3(pblocks), dim3(kBlock), 0, s2, w, inv);
         } else {
@@ -1276,7 +1263,14 @@ int launch(tpt_ctx* c, int mode, int flags, int spp, int64_t begin, int64_t stri
         // Shards larger than kWfChunk pixel streams run as consecutive chunks.
         const int64_t chunk = std::min(count, kWfChunk), last = count - (count - 1) / kWfChunk * kWfChunk;
         int rc = ensure_wf(c, std::max(chunk * wf_iters(chunk, spp), last * wf_iters(last, spp)));
-        if (rc) return rc;
+        if (rc) {
+            // not enough device memory for multi-iteration wavefronts (~19 KB per item):
+            // fall back to one iteration per wavefront (launch_bdpt_chunk caps nb at
+            // wf_cap / count), which needs a shard's worth of items only
+            (void)hipGetLastError();
+            rc = ensure_wf(c, chunk);
+            if (rc) return fail(c, TPT_E_ALLOC, "BDPT wavefront buffers: " + c->err);
+        }
         for (int64_t c0 = 0; c0 < count; c0 += kWfChunk) {
             rc = launch_bdpt_chunk(c, spp, dlist ? 0 : begin + c0 * stride, stride, std::min(kWfChunk, count - c0),
                                    dlist ? dlist + c0 : nullptr, dlist ? drows + 3 * c0 : drows, dsplat);

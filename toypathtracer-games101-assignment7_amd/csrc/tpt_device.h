@@ -480,8 +480,11 @@ struct QScratch {         // per wave, in LDS
     int32_t prim[kQC];
     uint32_t flag[64];    // shadow query: the owner's ray is blocked
 };
-TPT_D QScratch* wave_qs(const DScene& s) {  // wave index in an SGPR: no per-lane copy of the base is held
-    return reinterpret_cast<QScratch*>(s.qs) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+#ifndef TPT_QS_SGPR
+#define TPT_QS_SGPR 0  // 1: same-box A/B, Standard BDPT 441.0 -> 444.3 ms, bunny 256 spp 917 -> 923 ms
+#endif
+TPT_D QScratch* wave_qs(const DScene& s) {  // TPT_QS_SGPR: wave index in an SGPR, no per-lane copy of the base
+    return reinterpret_cast<QScratch*>(s.qs) + (TPT_QS_SGPR ? __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) : (threadIdx.x >> 6));
 }
 // LDS writes of some lanes made visible to reads of other lanes of the same wave
 TPT_D void wave_lds_sync() {
@@ -689,7 +692,10 @@ TPT_D bool shadow_flat_c(const DScene& s, const Ray& r, double thr, int cull) {
             sh = qs->flag[lane] != 0u;
         }
     }
-    for (int gi = 0; s.big && gi < s.ngroup; ++gi) {  // walk groups (any-hit: order is free)
+#ifndef TPT_DIAG_NO_GROUP_SHADOW
+#define TPT_DIAG_NO_GROUP_SHADOW 0  // diagnostics builds only (timing attribution; wrong images)
+#endif
+    for (int gi = 0; s.big && !TPT_DIAG_NO_GROUP_SHADOW && gi < s.ngroup; ++gi) {  // walk groups (any-hit: order is free)
         const DNode gn = s.groups[gi];
         if (gn.b >= 0) continue;
         const bool pass =

@@ -105,8 +105,16 @@ TPT_HD bool rcp_fast_ok(float x) {
 }
 
 // Vector.hpp:103-104 (see header note on the fma form)
+#ifndef TPT_DOT_OPAQUE
+#define TPT_DOT_OPAQUE 0
+#endif
 TPT_HD double dot3(V3 a, V3 b) {
 #if defined(__HIPCC__) && defined(__HIP_DEVICE_COMPILE__)
+#if TPT_DOT_OPAQUE
+    // opaque operands: the f64 conversions are made at each dot product instead of
+    // being shared between dot products and held (spilled) across the code in between
+    asm volatile("" : "+v"(a.x), "+v"(a.y), "+v"(a.z), "+v"(b.x), "+v"(b.y), "+v"(b.z));
+#endif
     double p = (double)a.x * (double)b.x;
     p = __builtin_fma((double)a.y, (double)b.y, p);
     return __builtin_fma((double)a.z, (double)b.z, p);

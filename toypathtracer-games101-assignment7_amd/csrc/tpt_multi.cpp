@@ -24,6 +24,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cmath>
 #include <cstring>
 #include <exception>
 #include <new>
@@ -293,7 +294,15 @@ int multi_render(tpt_multi* m, const tpt_render_params* p, float* rgb, float* sp
             st->samples += part[r].samples;
             st->bounces += part[r].bounces;
             st->nonfinite += part[r].nonfinite;  // shards are disjoint
+            st->nonfinite_splat += part[r].nonfinite_splat;
             st->kernel_ms = std::max(st->kernel_ms, part[r].kernel_ms);
+        }
+        if (splat && bdpt && n > 1) {
+            // splats of several devices land on the same pixels: count the reduced buffer
+            int64_t bad = 0;
+            for (int64_t p = 0; p < nf / 3; ++p)
+                bad += !(std::isfinite(splat[3 * p]) && std::isfinite(splat[3 * p + 1]) && std::isfinite(splat[3 * p + 2]));
+            st->nonfinite_splat = bad;
         }
         st->total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     }

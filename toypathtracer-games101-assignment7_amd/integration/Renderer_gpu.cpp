@@ -14,6 +14,7 @@
 // tests/test_gpu_parity.py::test_in_reference_binding runs it.
 #include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <iostream>
 #include <map>
 #include <vector>
@@ -40,7 +41,7 @@ struct GpuScene {
     tpt_scene_desc desc{};
 };
 
-void flatten(const Scene& scene, GpuScene& g) {
+bool flatten(const Scene& scene, GpuScene& g) {
     std::map<const Material*, int> ids;
     auto mat_id = [&](const Material* m) {
         auto it = ids.find(m);
@@ -75,7 +76,11 @@ void flatten(const Scene& scene, GpuScene& g) {
             t.center[2] = sp->center.z;
             t.radius = sp->radius;
         } else {
-            std::fprintf(stderr, "Renderer (GPU): unsupported object type\n");
+            // a bare Triangle or another Object subtype: the flattened scene would be
+            // wrong (and its emission lost), so the render is refused
+            std::fprintf(stderr, "Renderer (GPU): unsupported object type (Scene::objects[%zu]); not rendered\n",
+                         g.objs.size());
+            return false;
         }
         g.objs.push_back(t);
     }
@@ -93,6 +98,7 @@ void flatten(const Scene& scene, GpuScene& g) {
     d.objects = g.objs.data();
     d.num_vertices = (int64_t)g.verts.size() / 3;
     d.vertices = g.verts.data();
+    return true;
 }
 
 }  // namespace
@@ -103,23 +109,38 @@ void Renderer::Render(std::string outputFileName, const Scene& scene, int spp, i
     std::cout << "SPP: " << spp << "\n";
 
     GpuScene g;
-    flatten(scene, g);
+    if (!flatten(scene, g)) return;
+    if (tpt_abi_version() != TPT_ABI_VERSION) {
+        std::fprintf(stderr, "Renderer (GPU): libtpt ABI %d, built against %d\n", tpt_abi_version(), TPT_ABI_VERSION);
+        return;
+    }
     const size_t n = (size_t)scene.width * scene.height;
     std::vector<float> rgb(3 * n), splat(bdpt ? 3 * n : 0);
     tpt_stats st{};
-    tpt_ctx* ctx = nullptr;
-    int rc = tpt_create(0, &ctx);
-    if (rc == TPT_OK) rc = tpt_upload_scene(ctx, &g.desc);
-    if (rc == TPT_OK) {
-        const tpt_render_params p{spp, bdpt ? TPT_MODE_BDPT : TPT_MODE_PT, 0, 1, 0, 0};
-        rc = tpt_render(ctx, &p, rgb.data(), bdpt ? splat.data() : nullptr, &st);
-    }
-    if (rc != TPT_OK) {
-        std::fprintf(stderr, "Renderer (GPU): libtpt error %d: %s\n", rc, ctx ? tpt_last_error(ctx) : "no device");
+    const tpt_render_params p{spp, bdpt ? TPT_MODE_BDPT : TPT_MODE_PT, 0, 1, 0, 0};
+    // The reference's -j is CPU worker threads; the GPU count comes from TPT_GPUS
+    // (default 1).  With N > 1 the frame is sharded over devices 0..N-1 and reduced
+    // over RCCL (tpt_render_multi, the same split Renderer.cpp:86-114 makes over threads).
+    const char* ng = std::getenv("TPT_GPUS");
+    const int gpus = ng && *ng ? std::atoi(ng) : 1;
+    int rc;
+    if (gpus > 1) {
+        tpt_multi* m = nullptr;
+        rc = tpt_multi_create(gpus, nullptr, &m);
+        if (rc == TPT_OK) rc = tpt_multi_upload_scene(m, &g.desc);
+        if (rc == TPT_OK) rc = tpt_render_multi(m, &p, rgb.data(), bdpt ? splat.data() : nullptr, &st);
+        if (rc != TPT_OK) std::fprintf(stderr, "Renderer (GPU): libtpt error %d: %s\n", rc, tpt_multi_last_error(m));
+        tpt_multi_destroy(m);
+    } else {
+        tpt_ctx* ctx = nullptr;
+        rc = tpt_create(0, &ctx);
+        if (rc == TPT_OK) rc = tpt_upload_scene(ctx, &g.desc);
+        if (rc == TPT_OK) rc = tpt_render(ctx, &p, rgb.data(), bdpt ? splat.data() : nullptr, &st);
+        if (rc != TPT_OK)
+            std::fprintf(stderr, "Renderer (GPU): libtpt error %d: %s\n", rc, ctx ? tpt_last_error(ctx) : "no device");
         tpt_destroy(ctx);
-        return;
     }
-    tpt_destroy(ctx);
+    if (rc != TPT_OK) return;
 
     std::vector<Vector3f> framebuffer(n);
     for (size_t j = 0; j < n; ++j) framebuffer[j] = Vector3f(rgb[3 * j], rgb[3 * j + 1], rgb[3 * j + 2]);

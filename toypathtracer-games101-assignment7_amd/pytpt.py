@@ -13,6 +13,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("TPT_LIB") or os.path.join(HERE, "libtpt.so")  # TPT_LIB: profiling A/B only
 MODELS_DIR = os.path.join(HERE, "models")
+ABI_VERSION = 2  # TPT_ABI_VERSION of include/tpt.h
 
 TPT_OK = 0
 TPT_E_INVALID = -1
@@ -106,6 +107,8 @@ def lib():
     L.tpt_multi_last_error.restype = ctypes.c_char_p
     L.tpt_multi_upload_scene.argtypes = [P, ctypes.POINTER(SceneDesc)]
     L.tpt_render_multi.argtypes = [P, ctypes.POINTER(RenderParams), P, P, ctypes.POINTER(Stats)]
+    if L.tpt_abi_version() != ABI_VERSION:  # Stats is ABI 2's layout (include/tpt.h)
+        raise RuntimeError("%s has ABI %d, pytpt expects %d" % (LIB_PATH, L.tpt_abi_version(), ABI_VERSION))
     _lib = L
     return L
 
