@@ -61,6 +61,6 @@ if [ -f "$src/benchkt_$tag/run_kernel_stats.csv" ]; then
   cp "$src/benchkt_$tag/run_kernel_stats.csv" "profiles/${tag}_bench_kernel_stats.csv"
 fi
 if [ -f "$src/bench_$tag.log" ]; then
-  tail -1 "$src/bench_$tag.log" >> profiles/r03_bench_lines.jsonl
+  tail -1 "$src/bench_$tag.log" >> "profiles/${tag:0:3}_bench_lines.jsonl"
 fi
 echo "reduced $p into profiles/${tag}_*"
