@@ -6,7 +6,8 @@ tests/golden/frame_<cfg>.npz (tests/golden/make_frames.py; tests/frames.py).
     smooth dielectric at 4096 spp): the frame of the real Renderer::Render
     (Renderer.cpp:68-127), bit for bit -- sha256 of all 784*784*3 floats, and the
     non-finite pixel list.
-  * BDPT (configs[2] Standard 256 spp; configs[4]'s bunny scene at a reduced 256 spp):
+  * BDPT (configs[2] Standard 256 spp; configs[4]'s bunny scene at its own 4096 spp
+    (frame_c5, per-pixel route only) and at a reduced 256 spp (frame_c5r)):
     the per-pixel radiance (Renderer.cpp:49's fb accumulation of BDPT.cpp:282-315's
     t > 1 strategies) bit for bit; the t = 1 splat buffer (DrawToImage,
     SceneRenderingHelper.cpp:24-55) -- fp32 atomics here, per-worker sums in the
@@ -26,7 +27,7 @@ from frames import check_close, check_exact
 pytestmark = pytest.mark.gpu
 
 PT_FRAMES = ("c1", "c2", "c4_ball", "c4_smooth")
-BDPT_FRAMES = ("c3", "c5r")
+BDPT_FRAMES = ("c3", "c5r", "c5")
 MODES = {0: pytpt.MODE_PT, 1: pytpt.MODE_BDPT}
 
 
@@ -67,9 +68,11 @@ def test_bdpt_frame(ctx, cfg):
     what = "%s BDPT %d spp" % (g["preset"], g["spp"])
     check_exact(rgb, g, "rgb", what + " radiance")
     assert st.nonfinite == len(g["rgb_nonfinite"])
-    assert np.isfinite(splat).all() and st.nonfinite_splat == 0
+    if np.isfinite(g["splat_sum"]).all():
+        assert np.isfinite(splat).all() and st.nonfinite_splat == 0
     check_close(splat, g, "splat", what + " splats", 1e-4, 1e-4, 1e-3)
-    check_close(rgb + splat, g, "render", what + " radiance + splats vs Renderer::Render", 1e-4, 1e-4, 1e-3)
+    if "trace_only" not in g:  # frame_c5: the per-pixel route alone (make_frames.py TRACE_ONLY)
+        check_close(rgb + splat, g, "render", what + " radiance + splats vs Renderer::Render", 1e-4, 1e-4, 1e-3)
     tot = splat.astype(np.float64).sum((0, 1))
     # whole-frame splat energy: one fp32 buffer of atomics here, eight per-worker
     # buffers in the reference; observed 1.4e-5 relative at 256 spp
@@ -97,7 +100,7 @@ def test_pt_shards_sum_to_the_reference_frame(ctx, n):
     check_exact(tot, g, "rgb", "standard PT 1024 spp as %d shards" % n)
 
 
-@pytest.mark.parametrize("cfg", BDPT_FRAMES)
+@pytest.mark.parametrize("cfg", ("c3", "c5r"))
 def test_bdpt_eight_shards_sum_to_the_reference_frame(ctx, cfg):
     """configs[2] (and configs[4]'s scene at 256 spp) split as the 8-GPU run splits it:
     each stride-8 shard rendered alone -- at 1/8 of the frame a BDPT wavefront holds 16

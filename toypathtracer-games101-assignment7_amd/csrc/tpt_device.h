@@ -1352,9 +1352,15 @@ TPT_D V3 pt_sample(const DScene& s, PixPark px, uint32_t& rs) {
         const DMat& dm = s.mats[px.mat_index()];
         if (dm.has_em) result = result + v3(dm.em[0], dm.em[1], dm.em[2]);
     }
-    float pdf_b;
-    V3 wib = mat_sample(px.mat(s), px.v(kPxWo), px.shade(), &pdf_b, rs);
+    float pdf_b0;
+    const V3 wib0 = mat_sample(px.mat(s), px.v(kPxWo), px.shade(), &pdf_b0, rs);
     for (int li = 0; li < s.n_emitters; ++li) {
+        // opaque per-iteration copies of the BSDF sample: what the body derives from it
+        // (the ray's reciprocals, f64 conversions) is made here, not hoisted out of the
+        // emitter loop and held (spilled) across its queries -- Standard has one emitter
+        const V3 wib = opaque(wib0);
+        float pdf_b = pdf_b0;
+        asm volatile("" : "+v"(pdf_b));
         const DObj o = s.objs[s.emitters[li]];
         // DirectLightSampler::sample (PathTracer.cpp:26-40)
         V3 pc, pn;
