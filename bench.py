@@ -14,7 +14,9 @@ frame per step with the flattened scene already resident in HBM:
     N-GPU run would render, its kernel time, and T_full / (N * T_slowest_shard).
 --mode runs one workload alone (profiling runs use it).
 
-With N > 1 (launched by torch.distributed.run, one process per GPU) each rank
+`python bench.py --gpus N` (N > 1) without a launcher starts the N ranks itself: it
+counts the visible GPUs (exit 2 if fewer than N) and runs torch.distributed.run as a
+child process.  With N > 1 (one process per GPU) each rank
 renders its pixel shard (i = rank; i += N, the reference's own interleave,
 Renderer.cpp:38) into HBM and the [rgb; splat] buffer is summed onto rank 0 with one
 RCCL reduce over xGMI.  The frame is fixed as N grows: strong scaling.
@@ -30,7 +32,10 @@ duration measured live here (HIP events inside libtpt on the stream the kernel r
 on); `peak` = 1,024 SIMDs x the clock the profiled run held (GRBM_GUI_ACTIVE).
 roofline_hbm_model: SURVEY §8(d)'s modelled HBM yardstick (algorithmic scene-fetch
 bytes / kernel time / 8 TB/s); `traffic` is the measured memory-side bytes per launch
-(profiles/traffic.json).
+(profiles/traffic.json).  roofline_hbm_measured: those measured bytes (rocprofv3
+FETCH_SIZE / WRITE_SIZE of the profiled build) / the live kernel time / 8 TB/s.  An N-rank
+line adds `ranks` (device PCI ids, kernel and reduce ms per rank); every line ends with a
+compact per-config `summary`.
 
 cpu_baseline: the REAL reference renderer (oracle/_ref/libref.so, Renderer::Render
 with std::async threads, one per CPU this process may run on) on a bounded sample,
