@@ -174,3 +174,25 @@ def test_edge_full_frame_bdpt_1280x960():
     g = golden("edge_standard_1280x960.npz")
     img, _ = Oracle("standard", 1280, 960).render(1, 1, threads=1)
     assert eq_bits(blocks(img), g["bdpt1_blocks"])
+
+
+def test_frame_c5_crop_pixels_match_oracle():
+    """tests/golden/frame_c5.npz (configs[4], the bunny scene at its own 4096 spp, made by
+    the real reference's per-pixel route) against the CPU restatement on 12 pixels of
+    its full-resolution crops: the radiance bit for bit.  Bounded sample: ~1 s of
+    BDPT at 4096 spp per pixel on one core."""
+    import os
+    from conftest import GOLDEN
+    if not os.path.exists(os.path.join(GOLDEN, "frame_c5.npz")):
+        pytest.skip("frame_c5.npz not generated")
+    g = golden("frame_c5.npz")
+    assert int(g["spp"]) == 4096 and str(g["preset"]) == "bunny"
+    rng = np.random.default_rng(7)
+    pix, want = [], []
+    for ci, (r0, c0) in enumerate(g["crop_origins"]):
+        for _ in range(4):
+            dy, dx = rng.integers(0, 64, 2)
+            pix.append((r0 + dy) * 784 + (c0 + dx))
+            want.append(g["rgb_crops"][ci, dy, dx])
+    got = Oracle("bunny").trace_pixels(1, 4096, np.array(pix, np.int64))[0]
+    assert eq_bits(got, np.array(want, np.float32))
