@@ -862,6 +862,23 @@ __global__ __launch_bounds__(kBlock) void tpt_bdpt_out_kernel(WfState w, float* 
     out[3 * row + 2] = w.acc[3 * k + 2];
 }
 
+// Splat accumulation in stages (round 4).  t = 1 splats (DrawToImage) are fp32 atomics;
+// summed straight into one buffer over a 4096-spp frame, a bright pixel's sum reaches
+// ~1.4e5 and contributions below half an ulp of it (~0.004) are lost, a bias that grows
+// with spp: configs[4]'s frame came out 0.16 % low overall and 0.27 % low at the light
+// against the reference's own per-worker sums.  (The reference sums each worker's
+// splats in its own float buffer and merges the buffers after the join,
+// Renderer.cpp:86-114; the fold below does the same across groups of sample
+// iterations.)  Connect splats into a partial buffer, and every TPT_SPLAT_FOLD_SPP
+// iterations (and at the end) the partial sums are added into the caller's buffer and
+// cleared, in iteration order on the connect stream.
+__global__ void tpt_splat_fold_kernel(float* __restrict__ acc, float* __restrict__ part, int64_t n) {
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (int64_t)gridDim.x * blockDim.x) {
+        acc[k] = acc[k] + part[k];
+        part[k] = 0.0f;
+    }
+}
+
 __global__ void tpt_scale_kernel(float* __restrict__ buf, int64_t n, float spp) {
     const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k < n) buf[k] = buf[k] * 1.0f / spp;  // Renderer.cpp:59 `e * 1.0f / spp`
@@ -931,6 +948,8 @@ struct tpt_ctx {
     float* rgb = nullptr;
     float* splat = nullptr;
     int64_t fb_floats = 0;
+    float* splat_part = nullptr;  // BDPT: the splats of the last few wavefronts (folded into the caller's buffer)
+    int64_t part_floats = 0;
     int64_t* list = nullptr;
     int64_t list_cap = 0;
     float* rows = nullptr;
@@ -990,6 +1009,20 @@ int ensure_fb(tpt_ctx* c) {
     HIP_TRY(c, hipMalloc(&c->rgb, need * sizeof(float)));
     HIP_TRY(c, hipMalloc(&c->splat, need * sizeof(float)));
     c->fb_floats = need;
+    return TPT_OK;
+}
+
+// The partial splat buffer (W * H * 3 floats, zero between folds).
+int ensure_part(tpt_ctx* c) {
+    const int64_t need = (int64_t)c->hs.width * c->hs.height * 3;
+    if (c->part_floats < need) {
+        if (c->splat_part) (void)hipFree(c->splat_part);
+        c->splat_part = nullptr;
+        c->part_floats = 0;
+        HIP_TRY(c, hipMalloc(&c->splat_part, need * sizeof(float)));
+        HIP_TRY(c, hipMemsetAsync(c->splat_part, 0, need * sizeof(float), c->stream));
+        c->part_floats = need;
+    }
     return TPT_OK;
 }
 
@@ -1091,6 +1124,10 @@ int64_t shard_count(int64_t npix, int64_t begin, int64_t stride) {
 #ifndef TPT_GEN_GRID_Q_WALK2
 #define TPT_GEN_GRID_Q_WALK2 12  // ... when two gen kernels run at once (shards: wavefronts of >= 3 iterations)
 #endif
+#ifndef TPT_SPLAT_FOLD_SPP
+#define TPT_SPLAT_FOLD_SPP 64  // sample iterations per partial splat sum (tpt_splat_fold_kernel); one
+                               // buffer over 256 spp was within 1.4e-5 of the reference (frame_c5r)
+#endif
 #ifndef TPT_GEN2_MIN_NB
 #define TPT_GEN2_MIN_NB 3  // two gen streams when a wavefront holds >= this many iterations (whole frames,
                            // 2 iterations: one stream, bunny BDPT 256 spp 931.7 -> 919.2 ms, Standard 440.8 either way)
@@ -1190,12 +1227,17 @@ int launch_bdpt_chunk(tpt_ctx* c, int spp, int64_t begin, int64_t stride, int64_
         hipLaunchKernelGGL(tpt_bdpt_scatter_kernel, dim3(iblocks), dim3(kBlock), 0, gs[gsi], w, queue);
         HIP_TRY(c, hipEventRecord(c->ev_gen[b], gs[gsi]));
         HIP_TRY(c, hipStreamWaitEvent(s2, c->ev_gen[b], 0));
-        hipLaunchKernelGGL(conn_k, dim3(cblocks), dim3(kBlock), shmem, s2, c->ds, w, dsplat);
+        hipLaunchKernelGGL(conn_k, dim3(cblocks), dim3(kBlock), shmem, s2, c->ds, w, dsplat ? c->splat_part : nullptr);
         if (w.nb == 1) {
             hipLaunchKernelGGL(tpt_bdpt_fold_kernel, dim3(pblocks), dim3(kBlock), 0, s2, w, inv);
         } else {
             hipLaunchKernelGGL(tpt_bdpt_isum_kernel, dim3(iblocks), dim3(kBlock), 0, s2, w);
             hipLaunchKernelGGL(tpt_bdpt_fold_items_kernel, dim3(pblocks), dim3(kBlock), 0, s2, w, inv);
+        }
+        if (dsplat && ((it0 + w.nb) / TPT_SPLAT_FOLD_SPP > it0 / TPT_SPLAT_FOLD_SPP || it0 + w.nb >= spp)) {
+            const int64_t nf = (int64_t)c->hs.width * c->hs.height * 3;
+            hipLaunchKernelGGL(tpt_splat_fold_kernel, dim3((unsigned)std::min<int64_t>(4096, (nf + 255) / 256)), dim3(256), 0,
+                               s2, dsplat, c->splat_part, nf);
         }
         HIP_TRY(c, hipEventRecord(c->ev_fold[b], s2));
         if (it0 + w.nb >= spp) HIP_TRY(c, hipStreamWaitEvent(c->stream, c->ev_fold[b], 0));
@@ -1262,6 +1304,10 @@ int launch(tpt_ctx* c, int mode, int flags, int spp, int64_t begin, int64_t stri
 #endif
         // Shards larger than kWfChunk pixel streams run as consecutive chunks.
         const int64_t chunk = std::min(count, kWfChunk), last = count - (count - 1) / kWfChunk * kWfChunk;
+        if (dsplat) {
+            const int rp = ensure_part(c);
+            if (rp) return rp;
+        }
         int rc = ensure_wf(c, std::max(chunk * wf_iters(chunk, spp), last * wf_iters(last, spp)));
         if (rc) {
             // not enough device memory for multi-iteration wavefronts (~19 KB per item):
@@ -1389,7 +1435,7 @@ void tpt_destroy(tpt_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    for (void* p : {(void*)c->blob, (void*)c->rgb, (void*)c->splat, (void*)c->list, (void*)c->rows, (void*)c->counters,
+    for (void* p : {(void*)c->blob, (void*)c->rgb, (void*)c->splat, (void*)c->splat_part, (void*)c->list, (void*)c->rows, (void*)c->counters,
                     (void*)c->queue,
                     c->wf_mem, c->scan_tmp})
         if (p) (void)hipFree(p);

@@ -76,6 +76,14 @@ def lib():
         return _lib
     if not os.path.exists(LIB_PATH):
         raise RuntimeError("libtpt.so not built (run `make -C %s` or __graft_entry__.build())" % HERE)
+    # One HIP runtime per process: torch ships its own libamdhip64 and ROCr.  Loaded
+    # after libtpt had pulled in /opt/rocm's, torch finds no GPU ("No HIP GPUs are
+    # available") and RCCL cannot initialise; loaded first, libtpt binds to torch's
+    # runtime (same soname).  So torch, where installed, is loaded before libtpt.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = ctypes.CDLL(LIB_PATH)
     P = ctypes.c_void_p
     L.tpt_create.argtypes = [ctypes.c_int, ctypes.POINTER(P)]
