@@ -21,6 +21,7 @@
 #include "../../include/tpt.h"
 #include "tpt_bdpt.h"
 #include "tpt_device.h"
+#include "tpt_genseq.h"
 #include "tpt_scene_build.h"
 
 using namespace tpt;
@@ -564,8 +565,8 @@ __global__ __launch_bounds__(kBlock, TPT_GEN_MINWAVES) void tpt_bdpt_gen_kernel(
                 // one gen stream: gen(f - 1) completed before this kernel started, so a
                 // plain load sees its state; two: wait for its publication
                 const unsigned long long v = w.conc ? load_rngseq(w.rngseq, k) : w.rngseq[k];
-                if ((v >> 32) == (unsigned long long)batch) {
-                    rs = (uint32_t)v;
+                if (seq_ready(v, batch)) {
+                    rs = seq_state(v);
                     ready = true;
                 } else if (wait_t0 == 0) {
                     wait_t0 = (uint32_t)__builtin_amdgcn_s_memrealtime() | 1u;  // the wait starts
@@ -574,7 +575,7 @@ __global__ __launch_bounds__(kBlock, TPT_GEN_MINWAVES) void tpt_bdpt_gen_kernel(
                     // too, and report it.  Its items keep older contents, which are
                     // always a complete sample's (ensure_wf zeroes the arrays when it
                     // allocates them), so the scan, scatter and connect stay in bounds.
-                    store_rngseq(w.rngseq, k, (unsigned long long)(batch + 1) << 32 | 1u);
+                    store_rngseq(w.rngseq, k, seq_give_up(batch));
                     atomicOr(w.stall, 1);
                     k = -1;
                 }
@@ -609,7 +610,7 @@ __global__ __launch_bounds__(kBlock, TPT_GEN_MINWAVES) void tpt_bdpt_gen_kernel(
             if (++b < w.nb) {
                 fresh = true;  // the pixel's next sample, same stream, from the next step
             } else {
-                const unsigned long long v = (unsigned long long)(batch + 1) << 32 | rs;
+                const unsigned long long v = seq_publish(batch, rs);
                 if (TPT_DIAG_HOOKS && batch == 1 && k == w.drop_k) {
                     // diagnostics: k's state is never published, gen(2)'s watchdog takes over
                 } else if (w.conc) {
@@ -1193,7 +1194,7 @@ int launch_bdpt_chunk(tpt_ctx* c, int spp, int64_t begin, int64_t stride, int64_
     // resident workgroups to the other kernels.  (connect never waits; it frees its
     // slots as it finishes.)
     const int64_t resident = (int64_t)std::max(per_cu, 1) * std::max(c->num_cu, 1);
-    if (two_gen && 2 * (int64_t)gblocks > resident)
+    if (two_gen && !gen_grid_ok((long long)gblocks, (long long)resident))
         return fail(c, TPT_E_DEVICE, "BDPT: gen grid of " + std::to_string(gblocks) + " workgroups exceeds half of the " +
                                          std::to_string(resident) + " resident ones (two-stream hand-off invariant)");
     const float inv = 1.0f / spp;
