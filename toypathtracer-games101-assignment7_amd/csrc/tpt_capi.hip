@@ -1097,7 +1097,7 @@ int64_t shard_count(int64_t npix, int64_t begin, int64_t stride) {
 // whole frame / 1/8 shard): one frame 457.9 / 64.3 ms, two 445.6 / 61.9, three 442.5 /
 // 62.0, four 438.7 / 62.9 ms (47 GB); bunny BDPT 256 spp whole frame 940 / 933 / 928 /
 // 926 ms.
-#define TPT_WF_ITEMS 1229312
+#define TPT_WF_ITEMS 2458624  // round 4: four frames' worth (bunny 256 spp 801 -> 788 ms with the partition)
 #endif
 #ifndef TPT_WF_MIN_FRONTS
 // ... and at least this many wavefronts where spp allows (a wavefront's fill and drain
