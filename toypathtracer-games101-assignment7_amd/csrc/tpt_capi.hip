@@ -1112,7 +1112,9 @@ int64_t shard_count(int64_t npix, int64_t begin, int64_t stride) {
 // 1173, 10 -> 553 / 1131, 11 -> 556 / 1108, 12 -> 567 / -, 16 -> 585 / -.  Round 3,
 // wavefronts of two iterations: 10 -> 445.0 / 929.5, 11 -> 447.2 / 933.6, 12 -> 449.9 /
 // 932.6 ms.
-#define TPT_GEN_GRID_Q 10
+#define TPT_GEN_GRID_Q 10  // round 4, four-iteration wavefronts on two gen streams: 8 / 9 / 10 / 11 / 12 ->
+                           // 433.4 / 432.4 / 434.4 / 435.7 / 435.8 ms (Standard BDPT 256 spp); 9 took the
+                           // 1/8 shard from 61.6 to 63.9 ms, so 10 stays
 #endif
 #ifndef TPT_GEN_GRID_Q_WALK
 // ... for scenes with walk groups (the bunny), whose connect runs the walker partition:
@@ -1123,7 +1125,9 @@ int64_t shard_count(int64_t npix, int64_t begin, int64_t stride) {
 #define TPT_GEN_GRID_Q_WALK 12
 #endif
 #ifndef TPT_GEN_GRID_Q_WALK2
-#define TPT_GEN_GRID_Q_WALK2 12  // ... when two gen kernels run at once (shards: wavefronts of >= 3 iterations)
+#define TPT_GEN_GRID_Q_WALK2 11  // ... when two gen kernels run at once (wavefronts of >= 3 iterations: whole
+                                 // frames since round 4, and shards).  Bunny 256 spp, 10 / 11 / 12 / 13 ->
+                                 // 784.7 / 783.9 / 790.3 / 799.9 ms; 1/8 shard at 12 vs 10: 116.3 vs 117.2 ms
 #endif
 #ifndef TPT_SPLAT_FOLD_SPP
 #define TPT_SPLAT_FOLD_SPP 64  // sample iterations per partial splat sum (tpt_splat_fold_kernel); one
