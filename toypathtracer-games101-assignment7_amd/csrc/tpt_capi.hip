@@ -1033,6 +1033,12 @@ int ensure_part(tpt_ctx* c) {
 // items).
 int ensure_wf(tpt_ctx* c, int64_t n) {
     if (n <= c->wf_cap) return TPT_OK;
+#if TPT_DIAG_HOOKS
+    // diagnostics: refuse wavefront buffers above TPT_DIAG_WF_ITEMS_MAX items, as a failed
+    // hipMalloc would (drives launch()'s fallback to one iteration per wavefront)
+    if (const char* lim = std::getenv("TPT_DIAG_WF_ITEMS_MAX"))
+        if (*lim && n > std::atoll(lim)) return fail(c, TPT_E_ALLOC, "diagnostics: wavefront items above the limit");
+#endif
     if (c->wf_mem) (void)hipFree(c->wf_mem);
     if (c->scan_tmp) (void)hipFree(c->scan_tmp);
     c->wf_mem = c->scan_tmp = nullptr;
