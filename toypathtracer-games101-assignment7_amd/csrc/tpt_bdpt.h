@@ -370,14 +370,54 @@ TPT_D void rec_store_q(const WfState& w, int slot, int64_t k, float q1, float q8
 // P[j+2], folded into q1 / q8) is written as soon as P[j+2] exists, so only a
 // three-vertex window is live.  Same draws, vertices and float ops as the reference.
 // Returns false when the current subpath has ended: its vertex count is then i + 1.
-TPT_D bool gen_step(const DScene& s, const WfState& w, int64_t k, int& phase, BVert& prev, BVert& cur, int& i,
-                    uint32_t& rs) {
+// Deferred walks (round 4; walk-group scenes).  A lane whose extension ray passes the
+// walk group's box walks the mesh's tree; in a wave of persistent gen lanes only a few
+// need that at any one step, and the whole wave waits on their walks.  With kDefer a
+// lane that needs the walk while fewer than TPT_GEN_DEFER_MIN lanes of its wave do
+// parks the step half done -- the ray direction, the pdf and culling, and its closest
+// hit over the flat groups before the walk group (the DFS order) -- in its LDS slot
+// (GenDefer) and makes no progress this iteration; the parked lanes walk together a
+// few iterations later (when enough lanes want a walk, when one has waited
+// TPT_GEN_DEFER_MAX iterations, or when no other lane is active), then fold the flat
+// groups after the walk group and finish the step.  The lane's draws, operands, fold
+// order and stores are exactly the undeferred step's: only the time differs.
+#ifndef TPT_GEN_DEFER
+#define TPT_GEN_DEFER 1
+#endif
+#ifndef TPT_GEN_DEFER_MIN
+#define TPT_GEN_DEFER_MIN 24  // lanes wanting a walk before a wave walks
+#endif
+#ifndef TPT_GEN_DEFER_MAX
+#define TPT_GEN_DEFER_MAX 3  // iterations a parked lane waits at most
+#endif
+enum { kGdDx, kGdDy, kGdDz, kGdSr, kGdCl, kGdPrim, kGdDlo, kGdDhi, kGenDeferSlots };
+struct GenDefer {  // [slot][lane] in LDS
+    float* base;
+    TPT_D float& at(int slot) const { return base[slot * kBlock + threadIdx.x]; }
+};
+
+// One generation step (see the comment above gen_step's callers).  Returns 1 when the
+// subpath continues, 0 when it has ended (its vertex count is then i + 1), 2 when the
+// step was deferred (kDefer only; `pend` counts the iterations it has waited).
+template <bool kDefer>
+TPT_D int gen_step_t(const DScene& s, const WfState& w, int64_t k, int& phase, BVert& prev, BVert& cur, int& i,
+                     uint32_t& rs, int& pend, GenDefer dl, int gw) {
     const bool start = phase == 1;
     bool go = true;
     Ray ray;
     int cl = TPT_CULL_BACK;
     float sr = 0.0f;
-    if (start) {
+    Hit best;
+    best.prim = -1;
+    best.dist = 0.0;
+    const bool resumed = kDefer && pend != 0;
+    if (resumed) {
+        sr = dl.at(kGdSr);
+        cl = __float_as_int(dl.at(kGdCl));
+        best.prim = __float_as_int(dl.at(kGdPrim));
+        best.dist = __hiloint2double(__float_as_int(dl.at(kGdDhi)), __float_as_int(dl.at(kGdDlo)));
+        ray = make_ray(cur.x, v3(dl.at(kGdDx), dl.at(kGdDy), dl.at(kGdDz)));  // the same Ray as when parked
+    } else if (start) {
         const DObj lo = s.objs[s.emitters[0]];
         V3 pc, pn;
         int pp;
@@ -410,8 +450,70 @@ TPT_D bool gen_step(const DScene& s, const WfState& w, int64_t k, int& phase, BV
             }
         }
     }
-    if (!go) return false;
-    PTV it = scene_intersect(s, ray, cl);
+    if (!go) return 0;
+    PTV it;
+    if (!kDefer || gw < 0 || !(s.flat & kFlatHit) || !wave_finite(ray)) {
+        // Scene::Intersect as a whole (a parked lane's ray is finite, but another lane's
+        // may not be: the threaded walk then answers every lane, parked ones included,
+        // with the same result)
+        it = scene_intersect(s, ray, cl);
+        if (kDefer) pend = 0;
+    } else {
+        if (!resumed) {  // flat groups before the walk group, in the DFS order
+            int g0 = 0;
+            while (g0 < gw) {
+                int g1 = g0;
+                while (g1 < gw && s.groups[g1].b >= 0) ++g1;
+                if (g1 > g0) flat_closest_c(s, g0, g1, ray, cl, best);
+                if (g1 < gw) {  // another walk group (not deferred)
+                    const DNode gn = s.groups[g1];
+                    if (slab_hit_finite(gn.bmin[0], gn.bmin[1], gn.bmin[2], gn.bmax[0], gn.bmax[1], gn.bmax[2], ray))
+                        group_closest(s, gn, ray, cl, best);
+                    ++g1;
+                }
+                g0 = g1;
+            }
+        }
+        const DNode gn = s.groups[gw];
+        const bool need =
+            resumed || slab_hit_finite(gn.bmin[0], gn.bmin[1], gn.bmin[2], gn.bmax[0], gn.bmax[1], gn.bmax[2], ray);
+        const uint64_t nm = __ballot(need);
+        const bool walk_now = __popcll(nm) >= TPT_GEN_DEFER_MIN || __ballot(resumed && pend >= TPT_GEN_DEFER_MAX) != 0 ||
+                              __ballot(!need) == 0;
+        if (need && !walk_now) {
+            if (!resumed) {
+                dl.at(kGdDx) = ray.d.x; dl.at(kGdDy) = ray.d.y; dl.at(kGdDz) = ray.d.z;
+                dl.at(kGdSr) = sr;
+                dl.at(kGdCl) = __int_as_float(cl);
+                dl.at(kGdPrim) = __int_as_float(best.prim);
+                dl.at(kGdDlo) = __int_as_float(__double2loint(best.dist));
+                dl.at(kGdDhi) = __int_as_float(__double2hiint(best.dist));
+            }
+            pend = resumed ? pend + 1 : 1;
+            return 2;
+        }
+        if (need) group_closest(s, gn, ray, cl, best);
+        pend = 0;
+        int g0 = gw + 1;  // flat groups after the walk group
+        while (g0 < s.ngroup) {
+            int g1 = g0;
+            while (g1 < s.ngroup && s.groups[g1].b >= 0) ++g1;
+            if (g1 > g0) flat_closest_c(s, g0, g1, ray, cl, best);
+            if (g1 < s.ngroup) {
+                const DNode gm = s.groups[g1];
+                if (slab_hit_finite(gm.bmin[0], gm.bmin[1], gm.bmin[2], gm.bmax[0], gm.bmax[1], gm.bmax[2], ray))
+                    group_closest(s, gm, ray, cl, best);
+                ++g1;
+            }
+            g0 = g1;
+        }
+        it = ptv_bg();
+        if (best.prim >= 0) {
+            hit_geometry(s, ray, best, it.x, it.N);
+            it.type = T_MID;
+            it.prim = best.prim;
+        }
+    }
     const float pdf = srpdf_to_area(sr, cur.type, cur.x, cur.N, it.type, it.x, it.N);
     BVert nx;
     nx.x = it.x; nx.N = it.N; nx.type = it.type; nx.prim = it.prim;
@@ -426,9 +528,9 @@ TPT_D bool gen_step(const DScene& s, const WfState& w, int64_t k, int& phase, BV
         cur = nx;
         i = 1;
         phase = 2;
-        return !(sr == 0.0f && it.type == T_BG);
+        return !(sr == 0.0f && it.type == T_BG) ? 1 : 0;
     }
-    if (pdf == 0.0f) return false;
+    if (pdf == 0.0f) return 0;
     const V3 wo = normalized(prev.x - cur.x);
     const Mat m = load_mat(s, cur.mat);
     const float rr = i > 4 ? .8f : 1.f;
@@ -443,7 +545,12 @@ TPT_D bool gen_step(const DScene& s, const WfState& w, int64_t k, int& phase, BV
     prev = cur;
     cur = nx;
     ++i;
-    return true;
+    return 1;
+}
+TPT_D bool gen_step(const DScene& s, const WfState& w, int64_t k, int& phase, BVert& prev, BVert& cur, int& i,
+                    uint32_t& rs) {
+    int pend = 0;
+    return gen_step_t<false>(s, w, k, phase, prev, cur, i, rs, pend, GenDefer{nullptr}, -1) != 0;
 }
 
 struct GlobPaths {  // one pixel's paths in the HBM records

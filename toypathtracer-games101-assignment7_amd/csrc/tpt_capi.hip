@@ -489,6 +489,22 @@ __global__ __launch_bounds__(kBlock, TPT_GEN_MINWAVES) void tpt_bdpt_gen_kernel(
         __shared__ uint16_t wst[kWalkStack * kBlock];
         s.ws = wst;
     }
+    // deferred walks (gen_step_t): scenes with exactly one walk group
+    constexpr bool kDef = kSc == 2 && TPT_GEN_DEFER;
+    GenDefer dl{nullptr};
+    int gw = -1;
+    if constexpr (kDef) {
+        __shared__ float gdl[kGenDeferSlots * kBlock];
+        dl.base = gdl;
+        int nw = 0;
+        for (int gi = 0; gi < s.ngroup; ++gi)
+            if (s.groups[gi].b < 0) {
+                gw = gi;
+                ++nw;
+            }
+        if (nw != 1) gw = -1;
+    }
+    int pend = 0;  // iterations this lane's step has been parked (0: none)
     const int shard = blockIdx.x & 7;
     // pixel ordinals and items are < kWfChunk = 2^22: 32-bit indices in the loop
     const int nn = (int)w.n;
@@ -594,7 +610,7 @@ __global__ __launch_bounds__(kBlock, TPT_GEN_MINWAVES) void tpt_bdpt_gen_kernel(
         if (!run) continue;
         const int it = b * nn + k;
         int ln = -1;  // >= 0: the pixel's sample is complete
-        if (!gen_step(s, w, it, phase, prev, cur, i, rs)) {
+        if (gen_step_t<kDef>(s, w, it, phase, prev, cur, i, rs, pend, dl, gw) == 0) {
             if (phase == 0) {
                 cn = i + 1;
                 phase = 1;
