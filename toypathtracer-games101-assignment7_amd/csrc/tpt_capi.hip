@@ -1147,9 +1147,14 @@ int64_t shard_count(int64_t npix, int64_t begin, int64_t stride) {
 #define TPT_GEN_GRID_Q_WALK 12
 #endif
 #ifndef TPT_GEN_GRID_Q_WALK2
-#define TPT_GEN_GRID_Q_WALK2 11  // ... when two gen kernels run at once (wavefronts of >= 3 iterations: whole
-                                 // frames since round 4, and shards).  Bunny 256 spp, 10 / 11 / 12 / 13 ->
-                                 // 784.7 / 783.9 / 790.3 / 799.9 ms; 1/8 shard at 12 vs 10: 116.3 vs 117.2 ms
+#define TPT_GEN_GRID_Q_WALK2 10  // ... when two gen kernels run at once (wavefronts of >= 3 iterations: whole
+                                 // frames since round 4).  With the deferred walks, bunny 256 spp, 9 / 10 /
+                                 // 11 / 12 -> 742.0 / 742.1 / 753.9 / 760.4 ms
+#endif
+#ifndef TPT_GEN_GRID_Q_WALK_SHARD
+#define TPT_GEN_GRID_Q_WALK_SHARD 11  // ... and for wavefronts of >= 8 iterations (shards of a frame, whose gen
+                                      // lanes run many samples each): 1/8 shard 9 / 10 / 11 / 12 -> 110.2 /
+                                      // 108.5 / 106.8 / 107.5 ms
 #endif
 #ifndef TPT_SPLAT_FOLD_SPP
 #define TPT_SPLAT_FOLD_SPP 64  // sample iterations per partial splat sum (tpt_splat_fold_kernel); one
@@ -1203,7 +1208,10 @@ int launch_bdpt_chunk(tpt_ctx* c, int spp, int64_t begin, int64_t stride, int64_
 #ifndef TPT_CONN_GRID_WALK
 #define TPT_CONN_GRID_WALK 8192  // ... and scenes with walk groups (bunny BDPT 256 spp: 8192 / 16384 -> 928 / 935 ms)
 #endif
-    const int gen_q = c->sc == 2 ? (two_gen ? TPT_GEN_GRID_Q_WALK2 : TPT_GEN_GRID_Q_WALK) : TPT_GEN_GRID_Q;
+    const int gen_q = c->sc != 2 ? TPT_GEN_GRID_Q
+                      : !two_gen  ? TPT_GEN_GRID_Q_WALK
+                      : nb >= 8   ? TPT_GEN_GRID_Q_WALK_SHARD
+                                  : TPT_GEN_GRID_Q_WALK2;
     // persistent gen grid: as many workgroups as are resident at once, a multiple of
     // the 8 queue shards, and no more than the pixels need
     const auto gen_k = c->sc == 2 ? tpt_bdpt_gen_kernel<2> : c->sc == 1 ? tpt_bdpt_gen_kernel<1> : tpt_bdpt_gen_kernel<0>;
