@@ -459,21 +459,7 @@ TPT_D int gen_step_t(const DScene& s, const WfState& w, int64_t k, int& phase, B
         it = scene_intersect(s, ray, cl);
         if (kDefer) pend = 0;
     } else {
-        if (!resumed) {  // flat groups before the walk group, in the DFS order
-            int g0 = 0;
-            while (g0 < gw) {
-                int g1 = g0;
-                while (g1 < gw && s.groups[g1].b >= 0) ++g1;
-                if (g1 > g0) flat_closest_c(s, g0, g1, ray, cl, best);
-                if (g1 < gw) {  // another walk group (not deferred)
-                    const DNode gn = s.groups[g1];
-                    if (slab_hit_finite(gn.bmin[0], gn.bmin[1], gn.bmin[2], gn.bmax[0], gn.bmax[1], gn.bmax[2], ray))
-                        group_closest(s, gn, ray, cl, best);
-                    ++g1;
-                }
-                g0 = g1;
-            }
-        }
+        if (!resumed) closest_groups_c(s, 0, gw, ray, cl, best);  // the groups before the walk group
         const DNode gn = s.groups[gw];
         const bool need =
             resumed || slab_hit_finite(gn.bmin[0], gn.bmin[1], gn.bmin[2], gn.bmax[0], gn.bmax[1], gn.bmax[2], ray);
@@ -494,19 +480,7 @@ TPT_D int gen_step_t(const DScene& s, const WfState& w, int64_t k, int& phase, B
         }
         if (need) group_closest(s, gn, ray, cl, best);
         pend = 0;
-        int g0 = gw + 1;  // flat groups after the walk group
-        while (g0 < s.ngroup) {
-            int g1 = g0;
-            while (g1 < s.ngroup && s.groups[g1].b >= 0) ++g1;
-            if (g1 > g0) flat_closest_c(s, g0, g1, ray, cl, best);
-            if (g1 < s.ngroup) {
-                const DNode gm = s.groups[g1];
-                if (slab_hit_finite(gm.bmin[0], gm.bmin[1], gm.bmin[2], gm.bmax[0], gm.bmax[1], gm.bmax[2], ray))
-                    group_closest(s, gm, ray, cl, best);
-                ++g1;
-            }
-            g0 = g1;
-        }
+        closest_groups_c(s, gw + 1, s.ngroup, ray, cl, best);  // ... and after it
         it = ptv_bg();
         if (best.prim >= 0) {
             hit_geometry(s, ray, best, it.x, it.N);

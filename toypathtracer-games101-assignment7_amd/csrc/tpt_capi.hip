@@ -168,7 +168,9 @@ static_assert(kQ == 1 || kQ == 2 || kQ == 4 || kQ == 8 || kQ == 16, "Q must be a
 #define TPT_PT_SMALL_PIXELS 400000  // 32 lanes at 1/8 of the frame: 0.77 of linear vs 0.82 with 16
 #endif
 #ifndef TPT_PT_TAIL_WAVES
-#define TPT_PT_TAIL_WAVES 2  // pixel streams of the grid's 64-lane tail tier, in resident waves
+#define TPT_PT_TAIL_WAVES 1  // pixel streams of the grid's 64-lane tail tier, in resident waves (round 4:
+                             // 1 / 2 / 3 / 4 -> 1/8 shard 6.638 / 6.695 / 6.846 / 6.936 ms, whole frame
+                             // unchanged)
 #endif
 
 #ifndef TPT_PT_DPP

@@ -633,23 +633,27 @@ TPT_D void flat_closest_c(const DScene& s, int g0, int g1, const Ray& r, int cul
         wave_lds_sync();  // the next chunk reuses the slots
     }
 }
+// Closest hit over the groups [g0, g1) in the DFS order, folded into `best`: runs of
+// flat groups through the compacted query, split at walk groups, which are walked.
+TPT_D void closest_groups_c(const DScene& s, int g0, int g1, const Ray& r, int cull, Hit& best) {
+    while (g0 < g1) {
+        int ge = g0;
+        while (ge < g1 && !(s.big && s.groups[ge].b < 0)) ++ge;
+        if (ge > g0) flat_closest_c(s, g0, ge, r, cull, best);
+        if (ge < g1) {  // a walk group
+            const DNode gn = s.groups[ge];
+            if (slab_hit_finite(gn.bmin[0], gn.bmin[1], gn.bmin[2], gn.bmax[0], gn.bmax[1], gn.bmax[2], r))
+                group_closest(s, gn, r, cull, best);
+            ++ge;
+        }
+        g0 = ge;
+    }
+}
 TPT_D Hit traverse_flat_c(const DScene& s, const Ray& r, int cull) {
     Hit best;
     best.prim = -1;
     best.dist = 0.0;
-    int g0 = 0;
-    while (g0 < s.ngroup) {  // runs of flat groups, split at walk groups (the DFS order)
-        int g1 = g0;
-        while (g1 < s.ngroup && !(s.big && s.groups[g1].b < 0)) ++g1;
-        if (g1 > g0) flat_closest_c(s, g0, g1, r, cull, best);
-        if (g1 < s.ngroup) {  // a walk group
-            const DNode gn = s.groups[g1];
-            if (slab_hit_finite(gn.bmin[0], gn.bmin[1], gn.bmin[2], gn.bmax[0], gn.bmax[1], gn.bmax[2], r))
-                group_closest(s, gn, r, cull, best);
-            ++g1;
-        }
-        g0 = g1;
-    }
+    closest_groups_c(s, 0, s.ngroup, r, cull, best);
     return best;
 }
 // Shadow query (any hit with |hit - r.o|^2 < thr; r.o is the query's lc, see shadow_ray).
