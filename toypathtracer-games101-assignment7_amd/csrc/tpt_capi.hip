@@ -1120,8 +1120,13 @@ int64_t shard_count(int64_t npix, int64_t begin, int64_t stride) {
 // worth, ~24 GB of wavefront buffers.  Same-box shard model (Standard BDPT 256 spp,
 // whole frame / 1/8 shard): one frame 457.9 / 64.3 ms, two 445.6 / 61.9, three 442.5 /
 // 62.0, four 438.7 / 62.9 ms (47 GB); bunny BDPT 256 spp whole frame 940 / 933 / 928 /
-// 926 ms.
-#define TPT_WF_ITEMS 2458624  // round 4: four frames' worth (bunny 256 spp 801 -> 788 ms with the partition)
+// 926 ms.  Round 4: four frames (bunny 256 spp 801 -> 788 ms with the partition), then
+// six (~70 GB; same-box A/B at build b7f5ad7: bunny 256 spp 738.9 -> 729.8 ms, Standard
+// 435.9 -> 435.6 ms, bunny 4096 spp 1/8 shard 1621.8 -> 1621.7 ms).  Must stay < kWfChunk.
+#define TPT_WF_ITEMS 3687936
+#endif
+#if TPT_WF_ITEMS > (1 << 22)
+#error "TPT_WF_ITEMS must not exceed kWfChunk (32-bit item indices)"
 #endif
 #ifndef TPT_WF_MIN_FRONTS
 // ... and at least this many wavefronts where spp allows (a wavefront's fill and drain
