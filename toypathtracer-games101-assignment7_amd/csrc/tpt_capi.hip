@@ -735,7 +735,9 @@ TPT_D void conn_task(const DScene& s, const WfState& w, float* __restrict__ spla
 #define TPT_CONN_SORT 1  // 1: scenes with walk groups, 2: every scene, 0: off
 #endif
 #ifndef TPT_CONN_SORT_R
-#define TPT_CONN_SORT_R 8  // rounds of 64 tasks per partitioned chunk (round 4 end: 4 / 8 -> bunny 256 spp 745.7 / 735.6 ms, 1/8 shard 109.4 / 107.5 ms)
+#define TPT_CONN_SORT_R 16  // rounds of 64 tasks per partitioned chunk (4 / 8 -> bunny 256 spp 745.7 / 735.6 ms,
+                            // 1/8 shard 109.4 / 107.5 ms; at six-frame wavefronts 4 / 8 / 16 -> 740.6 / 725.3 /
+                            // 718.0 ms, 1/8 shard 8 / 16 -> 109.6 / 107.8 ms)
 #endif
 constexpr int kSortR = TPT_CONN_SORT_R;
 constexpr int kSortN = 64 * kSortR;
