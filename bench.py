@@ -240,18 +240,84 @@ def _free_port():
         return so.getsockname()[1]
 
 
+def visible_gpus(root=None):
+    """GPUs this process may open, counted WITHOUT the HIP runtime (the launcher must
+    not initialise the GPU before it starts the ranks): the kfd topology nodes that
+    have SIMDs and a DRM render node this user can open (/dev/dri/renderD<minor>, what
+    ROCr opens), capped by ROCR_/HIP_/CUDA_VISIBLE_DEVICES.  Returns (count, source),
+    or (None, reason) when there is no such view; then amdsmi is tried, and nothing
+    else: torch.cuda.device_count() may fall back to hipGetDeviceCount.
+    `root` (tests: TPT_BENCH_SYSFS_ROOT) prefixes /sys and /dev."""
+    root = root if root is not None else os.environ.get("TPT_BENCH_SYSFS_ROOT", "/")
+    base = os.path.join(root, "sys/class/kfd/kfd/topology/nodes")
+    n = None
+    try:
+        nodes = sorted((d for d in os.listdir(base) if d.isdigit()), key=int)
+    except OSError:
+        nodes = None
+    if nodes is not None:
+        n = 0
+        for nd in nodes:
+            props = {}
+            try:
+                with open(os.path.join(base, nd, "properties")) as f:
+                    for line in f:
+                        k, _, v = line.strip().partition(" ")
+                        props[k] = v.strip()
+            except OSError:
+                continue
+            if int(props.get("simd_count", "0") or 0) <= 0 or "drm_render_minor" not in props:
+                continue  # a CPU node
+            if os.access(os.path.join(root, "dev/dri/renderD%s" % props["drm_render_minor"]), os.R_OK | os.W_OK):
+                n += 1
+        source = "kfd topology"
+    elif root == "/" and not os.environ.get("TPT_BENCH_NO_AMDSMI"):
+        try:
+            import amdsmi
+            amdsmi.amdsmi_init()
+            try:
+                n = len(amdsmi.amdsmi_get_processor_handles())
+            finally:
+                amdsmi.amdsmi_shut_down()
+            source = "amdsmi"
+        except Exception as e:  # noqa: BLE001 -- any failure means "cannot count"
+            return None, "no kfd topology under %s and amdsmi failed (%s)" % (base, type(e).__name__)
+    else:
+        return None, "no kfd topology under %s" % base
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            n = min(n, len([x for x in v.split(",") if x.strip()]))
+    return n, source
+
+
+def check_distinct(line, world):
+    """An N-rank line must come from N different GPUs (distinct PCI ids of the ranks'
+    devices); returns the reason it does not, or None."""
+    if world <= 1 or "distinct_devices" not in line:
+        return None
+    if line["distinct_devices"] != world:
+        return "the %d ranks ran on %d distinct GPUs (PCI ids %s)" % (
+            world, line["distinct_devices"], sorted({str(r.get("pci_bus_id")) for r in line.get("ranks", [])}))
+    return None
+
+
 def spawn_ranks(a):
     """`bench.py --gpus N` (N > 1) run without a launcher: start N ranks through
     torch.distributed.run as a CHILD process (never an exec: this process may not
     replace itself once anything has touched the GPU) and return its exit code; rank
     0 prints the line.  Nothing here initialises the GPU: the visible devices are
-    counted with torch.cuda.device_count(), which on ROCm reads the device list only."""
+    counted from the kfd topology (visible_gpus), never through HIP; when they cannot be
+    counted that way the run is refused (exit 2)."""
     import subprocess
     if not a.rehearse:
-        import torch
-        n = torch.cuda.device_count()
+        n, source = visible_gpus()
+        if n is None:
+            print("bench.py: --gpus %d: cannot count GPUs without the HIP runtime (%s); start the ranks "
+                  "with torch.distributed.run instead" % (a.gpus, source), file=sys.stderr, flush=True)
+            return 2
         if n < a.gpus:
-            print("bench.py: --gpus %d needs %d visible GPUs, this box has %d" % (a.gpus, a.gpus, n),
+            print("bench.py: --gpus %d needs %d visible GPUs, this box has %d (%s)" % (a.gpus, a.gpus, n, source),
                   file=sys.stderr, flush=True)
             return 2
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(a.gpus),
@@ -559,7 +625,14 @@ def main():
         if shard_model is not None:
             out["shard_model"] = shard_model
         out["summary"] = summary(lines)
+        bad = check_distinct(out, r.world)
+        if bad:
+            out["distinct_devices_error"] = bad
         print(json.dumps(out), flush=True)
+        if bad:
+            print("bench.py: " + bad, file=sys.stderr, flush=True)
+            r.close()
+            sys.exit(3)
     r.close()
 
 

@@ -156,6 +156,11 @@ int tpt_create(int device, tpt_ctx** out);
 void tpt_destroy(tpt_ctx* ctx);
 const char* tpt_last_error(const tpt_ctx* ctx);
 int tpt_abi_version(void);
+/* The HIP version libtpt was compiled against (HIP_VERSION) and the one of the HIP
+ * runtime the process has loaded (hipRuntimeGetVersion; -1 if it cannot be read).  A
+ * process that loaded another libamdhip64 first (torch bundles its own) binds libtpt
+ * to that one: pytpt warns when the major versions differ. */
+void tpt_hip_versions(int* compiled, int* runtime);
 
 /* Build the two-level BVH exactly as the reference does (median split, BVH.cpp:30-99;
  * top level over objects, one BVH per mesh), flatten it and copy it to HBM. */

@@ -46,3 +46,20 @@ if gens:
             ce = max(ce, e)
     b2 += ce - cs
     print("gen|conn busy %.3f ms (%.1f %% of span)" % (b2 / 1e6, 100.0 * b2 / (t1 - t0)))
+    # sweep: time by the set of kernel kinds running (gen count, conn count)
+    pts = []
+    for s, e, n in ev:
+        kind = "g" if "gen_kernel" in n else "c" if "conn_kernel" in n else "o"
+        pts.append((s, 1, kind))
+        pts.append((e, -1, kind))
+    pts.sort()
+    cnt = {"g": 0, "c": 0, "o": 0}
+    acc = collections.defaultdict(int)
+    last = pts[0][0]
+    for t, d, kind in pts:
+        if t > last:
+            acc[(min(cnt["g"], 2), min(cnt["c"], 1), min(cnt["o"], 1))] += t - last
+        cnt[kind] += d
+        last = t
+    for key, v in sorted(acc.items(), key=lambda x: -x[1]):
+        print("gens=%d conn=%d other=%d : %8.3f ms (%.1f %%)" % (key + (v / 1e6, 100.0 * v / (t1 - t0))))

@@ -76,11 +76,20 @@ def check_exact(img, g, prefix, what):
 
 def check_close(img, g, prefix, what, tol_blocks, tol_crop_q99, tol_crop_max):
     """Frames that are sums of fp32 atomics (BDPT splats): 8x8 block means within
-    relative L2 tol_blocks, crop pixels within the given quantile / max."""
-    fin = np.isfinite(g[prefix + "_blocks"]).all(-1) & np.isfinite(block_means(img)).all(-1)
-    r = rel_l2_rows(block_means(img)[fin], g[prefix + "_blocks"][fin])
-    c = rel_l2_rows(crops(img, g["crop_origins"]), g[prefix + "_crops"])
-    c = c[np.isfinite(c)]
+    relative L2 tol_blocks, crop pixels within the given quantile / max.  Non-finite
+    values must sit where the reference's are: the blocks (and crop pixels) that are
+    non-finite in the pin and in img must be the same ones, and the finiteness mask of
+    the comparison comes from the pin alone, so a GPU NaN / Inf is a failure, never a
+    dropped block."""
+    gb, ib = g[prefix + "_blocks"], block_means(img)
+    fin = np.isfinite(gb).all(-1)
+    bad = np.nonzero(fin != np.isfinite(ib).all(-1))
+    assert bad[0].size == 0, (what, "non-finite 8x8 blocks differ from the reference's at", list(zip(*bad))[:10])
+    r = rel_l2_rows(ib[fin], gb[fin])
+    gc, ic = g[prefix + "_crops"], crops(img, g["crop_origins"])
+    cfin = np.isfinite(gc).all(-1)
+    assert np.array_equal(cfin, np.isfinite(ic).all(-1)), (what, "non-finite crop pixels differ from the reference's")
+    c = rel_l2_rows(ic[cfin], gc[cfin])
     print("%s: block relL2 max %.3g, crop relL2 q99 %.3g max %.3g" % (what, r.max(), np.quantile(c, 0.99), c.max()))
     assert r.max() <= tol_blocks, (what, r.max())
     assert np.quantile(c, 0.99) <= tol_crop_q99 and c.max() <= tol_crop_max, (what, np.quantile(c, 0.99), c.max())

@@ -68,8 +68,9 @@ def test_bdpt_frame(ctx, cfg):
     what = "%s BDPT %d spp" % (g["preset"], g["spp"])
     check_exact(rgb, g, "rgb", what + " radiance")
     assert st.nonfinite == len(g["rgb_nonfinite"])
-    if np.isfinite(g["splat_sum"]).all():
-        assert np.isfinite(splat).all() and st.nonfinite_splat == 0
+    # the device count of non-finite splat pixels agrees with the buffer; where they
+    # may sit is check_close's (non-finite blocks must be the reference's)
+    assert st.nonfinite_splat == int((~np.isfinite(splat.reshape(-1, 3)).all(1)).sum())
     check_close(splat, g, "splat", what + " splats", 1e-4, 1e-4, 1e-3)
     if "trace_only" not in g:  # frame_c5: the per-pixel route alone (make_frames.py TRACE_ONLY)
         check_close(rgb + splat, g, "render", what + " radiance + splats vs Renderer::Render", 1e-4, 1e-4, 1e-3)

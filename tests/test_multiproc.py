@@ -80,11 +80,13 @@ def test_shard_partition():
         sharding.shard(2, 2)
 
 
-def _bench(*args, timeout=240):
+def _bench(*args, timeout=240, env=None):
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    drop = ("WORLD_SIZE", "RANK", "LOCAL_RANK") + (
+        ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES") if env else ())
+    env = dict({k: v for k, v in os.environ.items() if k not in drop}, **(env or {}))
     return subprocess.run([sys.executable, os.path.join(root, "bench.py")] + list(args), capture_output=True,
                           text=True, timeout=timeout, env=env)
 
@@ -104,12 +106,61 @@ def test_bench_spawns_ranks_without_a_launcher():
     assert sum(r["pixels"] for r in line["ranks"]) == 64 * 64
 
 
-def test_bench_refuses_more_gpus_than_visible():
-    """On a box with fewer GPUs than --gpus the bench exits non-zero and names the
-    visible-device count (here: a CPU container, 0 devices)."""
-    import torch
-    if torch.cuda.device_count() >= 2:
-        pytest.skip("this box has 2+ GPUs")
-    p = _bench("--gpus", "2", "--steps", "1", "--warmup", "0", timeout=120)
-    assert p.returncode == 2
-    assert "visible GPUs, this box has %d" % torch.cuda.device_count() in p.stderr
+def _fake_sysfs(tmp_path, gpus, cpus=1, openable=None):
+    """A kfd topology tree with `cpus` CPU nodes and `gpus` GPU nodes (render minors
+    128, 129, ...), the first `openable` of whose render nodes exist."""
+    base = tmp_path / "sys/class/kfd/kfd/topology/nodes"
+    dri = tmp_path / "dev/dri"
+    dri.mkdir(parents=True)
+    node = 0
+    for _ in range(cpus):
+        (base / str(node)).mkdir(parents=True)
+        (base / str(node) / "properties").write_text("cpu_cores_count 64\nsimd_count 0\ndrm_render_minor 0\n")
+        node += 1
+    for g in range(gpus):
+        (base / str(node)).mkdir(parents=True)
+        (base / str(node) / "properties").write_text(
+            "cpu_cores_count 0\nsimd_count 1024\ngfx_target_version 90500\ndrm_render_minor %d\n" % (128 + g))
+        if openable is None or g < openable:
+            (dri / ("renderD%d" % (128 + g))).write_text("")
+        node += 1
+    return str(tmp_path)
+
+
+def test_visible_gpus_from_kfd_topology(tmp_path, monkeypatch):
+    """The launcher counts GPUs from the kfd topology and the render nodes it may open
+    (never through HIP), capped by the visibility variables (VERDICT r4 Next #5)."""
+    import bench
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        monkeypatch.delenv(var, raising=False)
+    root = _fake_sysfs(tmp_path, gpus=8, openable=3)
+    assert bench.visible_gpus(root) == (3, "kfd topology")
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "0,1")
+    assert bench.visible_gpus(root)[0] == 2
+    n, why = bench.visible_gpus(str(tmp_path / "nowhere"))
+    assert n is None and "no kfd topology" in why
+
+
+def test_bench_refuses_more_gpus_than_visible(tmp_path):
+    """On a box with fewer GPUs than --gpus the bench exits 2 and names the count."""
+    root = _fake_sysfs(tmp_path, gpus=1)
+    p = _bench("--gpus", "2", "--steps", "1", "--warmup", "0", timeout=120, env={"TPT_BENCH_SYSFS_ROOT": root})
+    assert p.returncode == 2, p.stderr[-2000:]
+    assert "needs 2 visible GPUs, this box has 1 (kfd topology)" in p.stderr
+
+
+def test_bench_refuses_when_gpus_cannot_be_counted(tmp_path):
+    """No kfd topology and no amdsmi: refuse (exit 2) rather than count through HIP."""
+    p = _bench("--gpus", "2", "--steps", "1", "--warmup", "0", timeout=120,
+               env={"TPT_BENCH_SYSFS_ROOT": str(tmp_path), "TPT_BENCH_NO_AMDSMI": "1"})
+    assert p.returncode == 2, p.stderr[-2000:]
+    assert "cannot count GPUs without the HIP runtime" in p.stderr
+
+
+def test_distinct_device_check():
+    """Rank 0 fails an N-rank line whose ranks did not run on N distinct GPUs."""
+    import bench
+    ranks = [{"rank": r, "pci_bus_id": "0000:%02x:00" % b} for r, b in enumerate((5, 5))]
+    assert bench.check_distinct({"ranks": ranks, "distinct_devices": 1}, 2).startswith("the 2 ranks ran on 1")
+    assert bench.check_distinct({"ranks": ranks, "distinct_devices": 2}, 2) is None
+    assert bench.check_distinct({"value": 1.0}, 1) is None

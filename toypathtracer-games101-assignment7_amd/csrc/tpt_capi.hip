@@ -439,6 +439,38 @@ __global__ __launch_bounds__(kBlock, TPT_PTI_MINWAVES) void tpt_pti_kernel(DScen
 #define TPT_CONN_MINWAVES 4  // waves per SIMD (measured: 4 beats 2, 3 and 5)
 #endif
 
+#ifndef TPT_GEN_STATS
+#define TPT_GEN_STATS 0  // diagnostics only: per-wave loop statistics of the gen kernels
+#endif
+#if TPT_GEN_STATS
+constexpr int kGenStatMax = 1 << 16;
+// per wave: kernel (0 queue, 1 resident) | launch ordinal << 8, step iterations, lane-steps, idle
+// iterations, real-time ticks (100 MHz)
+__device__ unsigned long long tpt_genstats[5 * kGenStatMax];
+__device__ unsigned tpt_genstat_n;
+struct GenStat {
+    unsigned long long it = 0, ls = 0, idle = 0, t0 = 0;
+    TPT_D void begin() { t0 = __builtin_amdgcn_s_memrealtime(); }
+    TPT_D void step(unsigned long long run) {
+        if (run) { ++it; ls += (unsigned long long)__popcll(run); } else { ++idle; }
+    }
+    TPT_D void end(int kind, int batch) {
+        if (lane_id() != 0) return;
+        const unsigned slot = atomicAdd(&tpt_genstat_n, 1u);
+        if (slot >= (unsigned)kGenStatMax) return;
+        unsigned long long* o = tpt_genstats + 5 * (size_t)slot;
+        o[0] = (unsigned long long)kind | ((unsigned long long)batch << 8);
+        o[1] = it; o[2] = ls; o[3] = idle; o[4] = __builtin_amdgcn_s_memrealtime() - t0;
+    }
+};
+#endif
+#ifndef TPT_WF_BUFS
+#define TPT_WF_BUFS 3  // BDPT wavefront buffers in flight.  Same-box shard model, 2 / 3 / 4:
+// 1/8-frame shards Standard BDPT 0.814 / 0.849 / 0.849 of linear, bunny 0.859 / 0.900 /
+// 0.898; whole frames unchanged (bunny 256 spp 1112 / 1089 / 1091 ms)
+#endif
+constexpr int kWfBufs = TPT_WF_BUFS;
+
 // Path generation, persistent: each lane runs a pixel's nb samples (the wavefront's
 // iterations) as a sequence of steps (start, camera-path vertex..., light start,
 // light-path vertex..., then the next sample of the same pixel) and takes the next
@@ -480,9 +512,13 @@ TPT_D void store_rngseq(unsigned long long* base, int k, unsigned long long v) {
     asm volatile("" : "+s"(base));
     __hip_atomic_store(base + k, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+#ifndef TPT_GEN_PRIO
+#define TPT_GEN_PRIO 0  // gen waves' issue priority (s_setprio) over connect's
+#endif
 template <int kSc>
 __global__ __launch_bounds__(kBlock, TPT_GEN_MINWAVES) void tpt_bdpt_gen_kernel(DScene s, WfState w, int batch,
                                                                                unsigned* __restrict__ queue) {
+    if (TPT_GEN_PRIO) __builtin_amdgcn_s_setprio(TPT_GEN_PRIO);
     stage_scene<kSc>(s);
     __shared__ QScratch qsm[kBlock / 64];  // compacted flat queries (tpt_device.h)
     s.qs = qsm;
@@ -521,22 +557,24 @@ __global__ __launch_bounds__(kBlock, TPT_GEN_MINWAVES) void tpt_bdpt_gen_kernel(
     bool drained = false;
     BVert prev, cur;
     // The camera vertices v0 / v1 of item (b, k): GenerateCameraPath's first two
-    // vertices (BDPT.cpp:41-59) do not depend on the sample (no jitter).  From the
-    // third wavefront of the chunk on, this buffer's slots 0/1 of every item still hold
-    // them (their q1/q8 may be stale; those of vertices cn-2, cn-1 are never read);
-    // before, sample 0 traces them and the later samples copy them from item (0, k).
+    // vertices (BDPT.cpp:41-59) do not depend on the sample (no jitter).  Items (b, k)
+    // with b < w.cam_nb were written by an earlier wavefront of the chunk in this buffer
+    // and their slots 0/1 still hold them (their q1/q8 may be stale; those of vertices
+    // cn-2, cn-1 are never read); otherwise sample 0 traces them (or finds them in
+    // item (0, k)) and the later samples copy them from item (0, k).
     auto start_sample = [&]() {
         const int it = b * nn + k;
         BVert c0, c1;
-        if (batch >= w.nbuf || b > 0) {
+        const bool cached = b < w.cam_nb;
+        if (cached || b > 0) {
             GlobPaths P;
-            P.rec = rec_at(w.rec, batch >= w.nbuf ? it : k, 0);
+            P.rec = rec_at(w.rec, cached ? it : k, 0);
             c0 = P.cam(0);
             c1 = P.cam(1);
         } else {
             camera_vertices(s, wf_pixel(w, k), c0, c1);
         }
-        if (batch < w.nbuf) {
+        if (!cached) {
             rec_store(w, 0, it, c0);
             rec_store(w, 1, it, c1);
         }
@@ -545,6 +583,10 @@ __global__ __launch_bounds__(kBlock, TPT_GEN_MINWAVES) void tpt_bdpt_gen_kernel(
         i = 1;
         phase = 0;
     };
+#if TPT_GEN_STATS
+    GenStat gst;
+    gst.begin();
+#endif
     bool ready = false;                 // k's stream state is in rs (its previous wavefront is done)
     bool fresh = false;                 // sample b of k starts at the top of the next step
     uint32_t wait_t0 = 0;               // when this lane started waiting for k (low 32 bits | 1; 0: not yet)
@@ -606,6 +648,9 @@ __global__ __launch_bounds__(kBlock, TPT_GEN_MINWAVES) void tpt_bdpt_gen_kernel(
         }
         if (__ballot(k >= 0) == 0) break;  // every lane idle and its shard drained
         const bool run = k >= 0 && ready;
+#if TPT_GEN_STATS
+        gst.step(__ballot(run));
+#endif
         // The whole wave waits on gen(f - 1): back off.  (No `continue` on this uniform
         // branch: that form of the loop spilled 120 B/lane instead of 52.)
         if (__ballot(run) == 0) __builtin_amdgcn_s_sleep(8);
@@ -641,7 +686,264 @@ __global__ __launch_bounds__(kBlock, TPT_GEN_MINWAVES) void tpt_bdpt_gen_kernel(
             }
         }
     }
+#if TPT_GEN_STATS
+    gst.end(0, batch);
+#endif
     atomicAdd(w.bounces, nbounce);
+}
+
+// Resident chains (round 5), for shards with no more pixel streams than a share of the
+// chip's resident lanes (1/8 of a 784 x 784 frame: 76,832 streams, 262,144 lanes).  In
+// the queue design above a pixel passes from gen(f) to gen(f + 1) every wavefront, so
+// its chain's current sample sits in one of two half-empty kernels and a SIMD issues
+// about twice the wave-iterations its chains need; at 1/8 of a frame the chains' serial
+// latency (a pixel's spp samples, one after the other: the RNG stream) bounds the shard.
+// Here ONE launch covers every wavefront of the chunk: lane k keeps pixel k and its
+// XorShift32 state for all spp samples and writes sample j into the buffer of its
+// wavefront f (f % kWfBufs), so waves stay dense.  Per lane, inside the loop:
+//   * before its first item of wavefront f >= kWfBufs it waits until fold(f - kWfBufs)
+//     has released that buffer (rfree[f - kWfBufs], set by tpt_bdpt_signal_kernel on
+//     the connect stream; the wait holds this lane only);
+//   * after its last item of wavefront f it counts itself into rdone[f] (an agent-scope
+//     release: its records are written back before the count can be seen), and the
+//     connect stream's tpt_bdpt_wait_kernel holds scan / scatter / connect / fold of
+//     wavefront f until rdone[f] == n.
+// A lane's draws, vertices and stores are the queue kernel's (same gen_step_t, same
+// sample order), so the frame is bit-identical.  No wait can block forever: wavefront
+// f - kWfBufs's items are made by lanes that wait on nothing later than f - kWfBufs, and
+// the connect stream never waits on gen's later wavefronts.  A watchdog (as in the queue
+// kernel) gives up a wait that does not finish, counts the lane into every remaining
+// rdone[] and flags the render.
+#ifndef TPT_GEN_RES_PUB
+// 1: a wave publishes wavefront f once, when its last lane leaves f: one release (XCD L2
+//    write-back) per wave and wavefront, plain stores; 0: every store write-through and
+//    each lane counts itself (measured slower: the write-through acks hold up the loads'
+//    waits)
+#define TPT_GEN_RES_PUB 1
+#endif
+#ifndef TPT_GEN_RES_PRIO
+#define TPT_GEN_RES_PRIO 0
+#endif
+#ifndef TPT_GEN_RES_SLEEP
+#define TPT_GEN_RES_SLEEP 127  // s_sleep units (64 cycles) between a waiting wave's polls
+#endif
+struct ResArgs {
+    const int2* wfi;    // per wavefront: (iterations, leading iterations whose items of its buffer hold the camera vertices)
+    int nf;             // wavefronts
+    int spp;
+    int64_t bstride;    // bytes from one wavefront buffer's arrays to the next one's (a multiple of 2 KB)
+    unsigned* rdone;    // per wavefront: pixel streams done with it
+    int* rfree;         // per wavefront: its buffer has been folded
+    float4* camv;       // per pixel stream: its camera vertex v1 (one record)
+    int lpw;            // pixel streams per wave (lanes lpw..63 of each wave idle)
+};
+template <int kSc>
+__global__ __launch_bounds__(kBlock, TPT_GEN_MINWAVES) void tpt_bdpt_gen_res_kernel(DScene s, WfState w, ResArgs a) {
+    // issue priority over connect's waves on the same SIMD: a chain's samples are serial,
+    // so its latency bounds the shard, and connect's waves fill the issue slots it leaves
+    if (TPT_GEN_RES_PRIO) __builtin_amdgcn_s_setprio(TPT_GEN_RES_PRIO);
+    stage_scene<kSc>(s);
+    __shared__ QScratch qsm[kBlock / 64];
+    s.qs = qsm;
+    s.ws = nullptr;
+    if constexpr (kSc == 2) {
+        __shared__ uint16_t wst[kWalkStack * kBlock];
+        s.ws = wst;
+    }
+    constexpr bool kDef = kSc == 2 && TPT_GEN_DEFER;
+    GenDefer dl{nullptr};
+    int gw = -1;
+    if constexpr (kDef) {
+        __shared__ float gdl[kGenDeferSlots * kBlock];
+        dl.base = gdl;
+        int nw = 0;
+        for (int gi = 0; gi < s.ngroup; ++gi)
+            if (s.groups[gi].b < 0) {
+                gw = gi;
+                ++nw;
+            }
+        if (nw != 1) gw = -1;
+    }
+    const int nn = (int)w.n;
+    // a.lpw streams per wave: sparser waves walk shorter (a wave's iteration lasts as long
+    // as its longest lane's step) and more of them hide each other's latency
+    int k = (int)((blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) * a.lpw + lane_id());
+    if (k >= nn || (int)lane_id() >= a.lpw) k = -1;
+    int f = 0, b = 0, j = 0;  // wavefront, iteration within it, sample
+    // item offset (in records) of wavefront g's buffer from buffer 0 (recomputed where
+    // used: held across the loop it spilled)
+    const int64_t rstride = a.bstride / (int64_t)(2 * kMaxLen * kRecV * sizeof(float4));
+    auto boff_of = [&](int g) { return (int64_t)(g % kWfBufs) * rstride; };
+    int phase = 0, i = 0, cn = 0, pend = 0;
+    uint32_t rs = 0;
+    unsigned long long nbounce = 0;
+    BVert prev, cur;
+    if (k >= 0) {
+        rs = (uint32_t)((int)wf_pixel(w, k) + 1);  // ResetRandom(i + 1), Renderer.cpp:42
+        for (int c = 0; c < 3; ++c) {
+            if (TPT_GEN_RES_PUB) w.acc[3 * k + c] = 0.0f;
+            else __hip_atomic_store(w.acc + 3 * k + c, 0.0f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    auto start_sample = [&]() {
+        const int64_t ir = (int64_t)b * nn + k + boff_of(f);
+        BVert c0, c1;
+        const bool cached = b < a.wfi[f].y;
+        if (cached || j > 0) {
+            // v0 is the camera itself (the same for every pixel), v1 the pixel's first hit
+            GlobPaths P;
+            P.rec = cached ? rec_at(w.rec, ir, 0) : a.camv + (int64_t)k * kRecV - kRecV;
+            c0 = camera_v0(s);
+            c1 = P.cam(1);
+        } else {
+            camera_vertices(s, wf_pixel(w, k), c0, c1);
+            float4* cv = a.camv + (int64_t)k * kRecV;
+            cv[0] = make_float4(c1.x.x, c1.x.y, c1.x.z, __builtin_bit_cast(float, tp_pack(c1.type, c1.prim)));
+            cv[1] = make_float4(c1.N.x, c1.N.y, c1.N.z, c1.pdf);
+            cv[2] = make_float4(c1.alpha.x, c1.alpha.y, c1.alpha.z, __builtin_bit_cast(float, c1.mat));
+            cv[3] = make_float4(c1.q1, c1.q8, 0.0f, 0.0f);
+        }
+        if (!cached) {
+            rec_store<!TPT_GEN_RES_PUB>(w, 0, ir, c0);
+            rec_store<!TPT_GEN_RES_PUB>(w, 1, ir, c1);
+        }
+        prev = c0;
+        cur = c1;
+        i = 1;
+        phase = 0;
+    };
+    bool fresh = k >= 0;   // sample j starts at the top of the next step
+    bool bok = true;       // wavefront f's buffer is free (f < kWfBufs: always)
+    uint32_t wait_t0 = 0;  // when this lane started waiting for it (| 1; 0: not yet)
+#if TPT_GEN_STATS
+    GenStat gst;
+    gst.begin();
+#endif
+    constexpr bool kWavePub = TPT_GEN_RES_PUB;
+    const unsigned nl0 = (unsigned)__popcll(__ballot(k >= 0));  // the wave's pixel streams
+    int pub = 0;           // (wave-uniform) the next wavefront this wave publishes
+    bool moved = false;    // this lane left a wavefront since the last publication check
+    // wave publication: every wavefront before the wave's slowest lane's is complete for
+    // the wave's nl0 streams; one release writes their records back, one lane counts them
+    auto publish = [&](int upto) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // keep: the fence's own wait may be dropped
+        if (lane_id() == (unsigned)__builtin_ctzll(__ballot(true)))
+            for (int g = pub; g < upto; ++g) __hip_atomic_fetch_add(a.rdone + g, nl0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        pub = upto;
+    };
+    for (;;) {
+        if (kWavePub && __ballot(moved) != 0) {
+            moved = false;
+            int fm = k >= 0 ? f : a.nf;
+            for (int o = 32; o >= 1; o >>= 1) fm = min(fm, __shfl_xor(fm, o));
+            if (fm > pub) publish(fm);
+        }
+        if (__ballot(k >= 0) == 0) break;
+        if (k >= 0 && !bok) {
+            // relaxed (sc1) poll: gen reads nothing the connect stream wrote, it only must
+            // not overwrite the buffer before connect and fold are done with it
+            bok = __hip_atomic_load(a.rfree + (f - kWfBufs), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+            if (bok) {
+                wait_t0 = 0;
+            } else if (wait_t0 == 0) {
+                wait_t0 = (uint32_t)__builtin_amdgcn_s_memrealtime() | 1u;
+            } else if (TPT_WATCHDOG && (uint32_t)__builtin_amdgcn_s_memrealtime() - wait_t0 > w.stall_ticks) {
+                atomicOr(w.stall, 1);
+                if (kWavePub) {
+                    f = a.nf;  // the wave counts this stream into every remaining wavefront
+                    moved = true;
+                } else {
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    for (int g = f; g < a.nf; ++g) __hip_atomic_fetch_add(a.rdone + g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+                k = -1;
+            }
+        }
+        const bool run = k >= 0 && bok;
+#if TPT_GEN_STATS
+        gst.step(__ballot(run));
+#endif
+        if (run && fresh) {  // one call site: camera_vertices is inlined once
+            start_sample();
+            fresh = false;
+        }
+        // the whole wave waits for a buffer: back off long (thousands of waves polling a few
+        // flags every 512 cycles took a large share of the memory system)
+        if (__ballot(run) == 0) __builtin_amdgcn_s_sleep(TPT_GEN_RES_SLEEP);
+        if (!run) continue;
+        const int64_t ir = (int64_t)b * nn + k + boff_of(f);
+        int ln = -1;
+        if (gen_step_t<kDef, !kWavePub>(s, w, ir, phase, prev, cur, i, rs, pend, dl, gw) == 0) {
+            if (phase == 0) {
+                cn = i + 1;
+                phase = 1;
+            } else {
+                ln = i + 1;
+            }
+        }
+        if (ln >= 0) {
+            const int64_t it = (int64_t)b * nn + k, eo = (int64_t)(f % kWfBufs) * a.bstride;
+            int* cnt = reinterpret_cast<int*>(reinterpret_cast<char*>(w.cnt) + eo);
+            unsigned long long* np = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(w.np) + eo);
+            unsigned long long* np2 = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(w.np2) + eo);
+            const int cv = cn | (ln << 16);
+            const unsigned long long v1 = (unsigned long long)(cn - 1) | ((unsigned long long)((cn - 1) * (ln - 1)) << 32),
+                                     v2 = (unsigned long long)(cn - 1) | ((unsigned long long)ln << 32);
+            if (kWavePub) {
+                cnt[it] = cv;
+                np[it] = v1;
+                np2[it] = v2;
+            } else {
+                __hip_atomic_store(cnt + it, cv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(np + it, v1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(np2 + it, v2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            nbounce += (unsigned long long)(cn + ln);
+            ++j;
+            if (++b == a.wfi[f].x) {  // the lane's last item of wavefront f: hand it to connect
+                if (kWavePub) {
+                    moved = true;
+                } else {
+                    // every store of the hand-off was write-through: drained, they are in
+                    // memory, and a relaxed count publishes them (no L2 write-back)
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    __hip_atomic_fetch_add(a.rdone + f, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+                ++f;
+                b = 0;
+                bok = f < kWfBufs;
+            }
+            if (j >= a.spp) k = -1;
+            else fresh = true;
+        }
+    }
+    if (kWavePub && pub < a.nf) publish(a.nf);
+#if TPT_GEN_STATS
+    gst.end(1, 0);
+#endif
+    atomicAdd(w.bounces, nbounce);
+}
+
+// The connect stream's gate for a resident-chains wavefront: one lane waits until every
+// pixel stream has counted itself into *done (or the watchdog fires: the render is then
+// flagged, and what runs after it reads complete older samples, in bounds).
+__global__ void tpt_bdpt_wait_kernel(const unsigned* done, unsigned n, int* stall, unsigned ticks) {
+    if (threadIdx.x != 0) return;
+    const uint32_t t0 = (uint32_t)__builtin_amdgcn_s_memrealtime();
+    // relaxed poll: the kernels after this one read the wavefront, and each starts with
+    // its own acquire
+    while (__hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < n) {
+        __builtin_amdgcn_s_sleep(32);
+        if (TPT_WATCHDOG && (uint32_t)__builtin_amdgcn_s_memrealtime() - t0 > ticks) {
+            atomicOr(stall, 2);
+            break;
+        }
+    }
+}
+// ... and its release of a folded wavefront's buffer to the resident gen kernel.
+__global__ void tpt_bdpt_signal_kernel(int* flag) {
+    if (threadIdx.x == 0) __hip_atomic_store(flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 
@@ -947,12 +1249,6 @@ __global__ __launch_bounds__(kBlock) void tpt_intersect_kernel(DScene s, const f
 #define TPT_BDPT_SERIAL 0  // 1: connect / fold on the gen stream (per-kernel timing builds only)
 #endif
 
-#ifndef TPT_WF_BUFS
-#define TPT_WF_BUFS 3  // BDPT wavefront buffers in flight.  Same-box shard model, 2 / 3 / 4:
-// 1/8-frame shards Standard BDPT 0.814 / 0.849 / 0.849 of linear, bunny 0.859 / 0.900 /
-// 0.898; whole frames unchanged (bunny 256 spp 1112 / 1089 / 1091 ms)
-#endif
-constexpr int kWfBufs = TPT_WF_BUFS;
 // per wavefront buffer: gen's 8 shard counters, 64 B apart
 constexpr size_t kQueueBytes = kWfBufs * 8 * 64;
 static_assert(kWfBufs >= 2 && kWfBufs <= 4, "2 to 4 wavefront buffers");
@@ -982,6 +1278,15 @@ struct tpt_ctx {
     // wavefront BDPT state (sized for wf_cap pixels)
     void* wf_mem = nullptr;
     int64_t wf_cap = 0;
+    int64_t wf_stride = 0;            // bytes from one wavefront buffer's arrays to the next one's
+    void* res_mem = nullptr;          // resident-chains gen: per-wavefront counters + camera vertices
+    int64_t res_bytes = 0;
+    std::vector<int2> res_wfi;        // host copy of the per-wavefront (iterations, cached) table
+    bool no_resident = false;         // the resident-chains path timed out once on this context: not used again
+    bool resident_used = false;       // the current render used it
+    int64_t wf_failed = 0;            // a wavefront allocation of this many items failed (0: none);
+                                      // later renders of the same shard size do not retry it
+    int64_t wf_failed_count = 0;      // ... for shards of this many pixel streams
     WfState wf[kWfBufs]{};            // kWfBufs wavefront buffers: gen(f+1..) overlaps connect(f)
     hipStream_t stream2 = nullptr;    // connect + fold
     hipStream_t stream3 = nullptr;    // gen / scan / scatter of the odd wavefronts (even ones: stream)
@@ -1041,9 +1346,12 @@ int ensure_part(tpt_ctx* c) {
         c->splat_part = nullptr;
         c->part_floats = 0;
         HIP_TRY(c, hipMalloc(&c->splat_part, need * sizeof(float)));
-        HIP_TRY(c, hipMemsetAsync(c->splat_part, 0, need * sizeof(float), c->stream));
         c->part_floats = need;
     }
+    // cleared at the start of every render (before its first kernel, on the stream every
+    // launch follows): a render that failed between a connect and its fold must not leave
+    // partial splats behind for the next one (~7 MB, negligible beside a frame)
+    HIP_TRY(c, hipMemsetAsync(c->splat_part, 0, need * sizeof(float), c->stream));
     return TPT_OK;
 }
 
@@ -1067,13 +1375,18 @@ int ensure_wf(tpt_ctx* c, int64_t n) {
     auto al = [](int64_t b) { return (b + 255) & ~(int64_t)255; };
     const int64_t b_rec = al(2 * kMaxLen * kRecV * n * 16), b_i = al(n * 4), b_l = al(n * 8),
                   b_own = al(n * maxs * 4), b_res = al(n * maxs * 12), b_acc = al(n * 12);
-    const int64_t per_buf = b_rec + b_i + 4 * b_l + b_own + b_res + b_acc;
+    // per buffer: a multiple of one item's records (2 KB), so that buffer b's arrays sit at
+    // the same element offsets from buffer 0's (the resident gen kernel addresses them so)
+    const int64_t rec_item = 2 * kMaxLen * kRecV * 16;
+    const int64_t per_buf = (b_rec + b_i + 4 * b_l + b_own + b_res + b_acc + rec_item - 1) / rec_item * rec_item;
     const int64_t total = kWfBufs * per_buf + b_l + b_acc;
     HIP_TRY(c, hipMalloc(&c->wf_mem, total));
 
     char* p = (char*)c->wf_mem;
+    c->wf_stride = per_buf;
     for (int b = 0; b < kWfBufs; ++b) {
         WfState& w = c->wf[b];
+        p = (char*)c->wf_mem + b * per_buf;
         w.rec = (float4*)p; p += b_rec;
         w.cnt = (int*)p; p += b_i;
         w.np = (unsigned long long*)p; p += b_l;
@@ -1084,6 +1397,7 @@ int ensure_wf(tpt_ctx* c, int64_t n) {
         w.res = (float*)p; p += b_res;
         w.isum = (float*)p; p += b_acc;
     }
+    p = (char*)c->wf_mem + kWfBufs * per_buf;
     for (int b = 0; b < kWfBufs; ++b) c->wf[b].rngseq = (unsigned long long*)p;
     p += b_l;
     // Every item's (cnt, np, np2) starts as a valid empty sample, so a wavefront whose
@@ -1178,6 +1492,158 @@ int wf_iters(int64_t count, int spp) {
     return (int)std::min<int64_t>(nb, std::max(1, spp / TPT_WF_MIN_FRONTS));
 }
 
+#ifndef TPT_WF_RAMP
+#define TPT_WF_RAMP 2  // ramp steps at each end of the wavefront schedule (0: uniform; 2 / 3 / 4 -> bunny BDPT 256 spp
+                       // 718.1 -> 715.2 / 716.2 / 715.9 ms, Standard 432.1 -> 430.1 / 431.0 / 429.8 ms, same box)
+#endif
+// Sample iterations of each wavefront of a chunk.  Connect(f) starts only when gen(f)
+// is complete, so the first gen runs with nothing beside it and the last connect runs
+// alone.  With TPT_WF_RAMP = R the schedule starts and ends with wavefronts of nb >> R,
+// ..., nb >> 1 iterations (the pipeline fills and drains in short steps), and the
+// iterations in between are split into wavefronts of at most nb, as even as possible.
+// Uniform (nb, ..., nb, remainder) when R = 0 or spp is too small for the ramps.
+std::vector<int> wf_schedule(int spp, int nb) {
+    std::vector<int> ramp;
+    for (int r = TPT_WF_RAMP; r >= 1; --r) {
+        const int v = std::max(1, nb >> r);
+        if (v < nb && (ramp.empty() || v > ramp.back())) ramp.push_back(v);
+    }
+    int rs = 0;
+    for (int v : ramp) rs += 2 * v;
+    std::vector<int> out;
+    if (ramp.empty() || spp < rs + nb) {
+        for (int it0 = 0; it0 < spp; it0 += nb) out.push_back(std::min(nb, spp - it0));
+        return out;
+    }
+    out = ramp;
+    const int mid = spp - rs, m = (mid + nb - 1) / nb;
+    for (int j = 0; j < m; ++j) out.push_back(mid / m + (j < mid % m ? 1 : 0));
+    out.insert(out.end(), ramp.rbegin(), ramp.rend());
+    return out;
+}
+
+#ifndef TPT_GEN_RES
+#define TPT_GEN_RES 0  // resident-chains gen (tpt_bdpt_gen_res_kernel) for small shards (off: see DESIGN §5.2)
+#endif
+#ifndef TPT_GEN_RES_LPW
+#define TPT_GEN_RES_LPW 32  // ... with this many pixel streams per wave
+#endif
+#ifndef TPT_GEN_RES_Q
+#define TPT_GEN_RES_Q 12  // ... for shards whose waves take at most this many 32nds of the chip's resident ones
+#endif
+#ifndef TPT_CONN_GRID
+#define TPT_CONN_GRID 16384  // connect's grid-stride grid, small flat scenes (Standard BDPT 256 spp: 8192 / 16384 -> 445.4 / 441.2 ms)
+#endif
+#ifndef TPT_CONN_GRID_WALK
+#define TPT_CONN_GRID_WALK 8192  // ... and scenes with walk groups (bunny BDPT 256 spp: 8192 / 16384 -> 928 / 935 ms)
+#endif
+
+// The per-wavefront chain on the connect stream s2: scan, scatter, connect, strategy sums
+// and fold, the periodic splat fold; `it0` is the wavefront's first sample iteration.
+int launch_wavefront_tail(tpt_ctx* c, hipStream_t s2, const WfState& w, void* scan_tmp, int it0, int spp, float inv,
+                          float* dsplat) {
+    const size_t shmem = (size_t)c->ds.lds_bytes;
+    const unsigned iblocks = (unsigned)((w.ni + kBlock - 1) / kBlock), pblocks = (unsigned)((w.n + kBlock - 1) / kBlock);
+    const unsigned cblocks = (unsigned)std::min<int64_t>(c->sc == 2 ? TPT_CONN_GRID_WALK : TPT_CONN_GRID,
+                                                         (w.ni * 24 + kBlock - 1) / kBlock + 1);
+    const auto conn_k = c->sc == 2 ? tpt_bdpt_conn_kernel<2> : c->sc == 1 ? tpt_bdpt_conn_kernel<1> : tpt_bdpt_conn_kernel<0>;
+    size_t bytes = c->scan_bytes;
+    HIP_TRY(c, rocprim::inclusive_scan(scan_tmp, bytes, w.np, w.incl, (size_t)w.ni, rocprim::plus<unsigned long long>(), s2));
+    bytes = c->scan_bytes;
+    HIP_TRY(c, rocprim::inclusive_scan(scan_tmp, bytes, w.np2, w.incl2, (size_t)w.ni, rocprim::plus<unsigned long long>(), s2));
+    hipLaunchKernelGGL(tpt_bdpt_scatter_kernel, dim3(iblocks), dim3(kBlock), 0, s2, w, c->queue);
+    hipLaunchKernelGGL(conn_k, dim3(cblocks), dim3(kBlock), shmem, s2, c->ds, w, dsplat ? c->splat_part : nullptr);
+    if (w.nb == 1) {
+        hipLaunchKernelGGL(tpt_bdpt_fold_kernel, dim3(pblocks), dim3(kBlock), 0, s2, w, inv);
+    } else {
+        hipLaunchKernelGGL(tpt_bdpt_isum_kernel, dim3(iblocks), dim3(kBlock), 0, s2, w);
+        hipLaunchKernelGGL(tpt_bdpt_fold_items_kernel, dim3(pblocks), dim3(kBlock), 0, s2, w, inv);
+    }
+    if (dsplat && ((it0 + w.nb) / TPT_SPLAT_FOLD_SPP > it0 / TPT_SPLAT_FOLD_SPP || it0 + w.nb >= spp)) {
+        const int64_t nf = (int64_t)c->hs.width * c->hs.height * 3;
+        hipLaunchKernelGGL(tpt_splat_fold_kernel, dim3((unsigned)std::min<int64_t>(4096, (nf + 255) / 256)), dim3(256), 0,
+                           s2, dsplat, c->splat_part, nf);
+    }
+    return TPT_OK;
+}
+
+// Resident chains (tpt_bdpt_gen_res_kernel): one gen launch for the whole chunk on
+// c->stream, one lane per pixel stream; per wavefront f on the connect stream: wait for
+// rdone[f] == count, the wavefront's tail, then release its buffer (rfree[f]).  Needs the
+// two streams to run concurrently (distinct hardware queues, as a context's streams are
+// when it is created with fewer than GPU_MAX_HW_QUEUES - 2 other streams in the process);
+// otherwise gen's first buffer wait times out (watchdog), the render fails with
+// TPT_E_DEVICE and the context stops using this path.
+int launch_bdpt_resident(tpt_ctx* c, int spp, int64_t begin, int64_t stride, int64_t count, const int64_t* dlist,
+                         float* drows, float* dsplat, int nb) {
+    const size_t shmem = (size_t)c->ds.lds_bytes;
+    hipStream_t s2 = c->stream2;
+    const std::vector<int> sched = wf_schedule(spp, nb);
+    const int nf = (int)sched.size();
+    c->res_wfi.assign(nf, int2{0, 0});
+    int cam_nb[kWfBufs] = {};
+    for (int f = 0; f < nf; ++f) {
+        const int b = f % kWfBufs;
+        c->res_wfi[f] = int2{sched[f], cam_nb[b]};
+        cam_nb[b] = std::max(cam_nb[b], sched[f]);
+    }
+    auto al = [](int64_t x) { return (x + 255) & ~(int64_t)255; };
+    const int64_t need = al((int64_t)nf * 8) + 2 * al((int64_t)nf * 4) + count * kRecV * 16;
+    if (c->res_bytes < need) {
+        if (c->res_mem) (void)hipFree(c->res_mem);
+        c->res_mem = nullptr;
+        c->res_bytes = 0;
+        HIP_TRY(c, hipMalloc(&c->res_mem, need));
+        c->res_bytes = need;
+    }
+    char* p = (char*)c->res_mem;
+    int2* wfi = (int2*)p;
+    p += al((int64_t)nf * 8);
+    unsigned* rdone = (unsigned*)p;
+    int* rfree = (int*)(p + al((int64_t)nf * 4));
+    float4* camv = (float4*)(p + 2 * al((int64_t)nf * 4));
+    HIP_TRY(c, hipMemcpyAsync(wfi, c->res_wfi.data(), (size_t)nf * sizeof(int2), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, hipMemsetAsync(rdone, 0, (size_t)(2 * al((int64_t)nf * 4)), c->stream));
+    HIP_TRY(c, hipEventRecord(c->ev_start, c->stream));
+    HIP_TRY(c, hipStreamWaitEvent(s2, c->ev_start, 0));
+    auto prep = [&](WfState w, int nbf) {
+        w.list = dlist;
+        w.begin = begin;
+        w.stride = stride;
+        w.n = count;
+        w.nb = nbf;
+        w.ni = (int64_t)nbf * count;
+        w.bounces = c->counters;
+        w.stall = reinterpret_cast<int*>(c->counters + 4);
+        w.stall_ticks = c->stall_ticks;
+        w.drop_k = c->drop_k;
+        w.conc = 0;
+        w.cam_nb = 0;
+        return w;
+    };
+    const unsigned pblocks = (unsigned)((count + kBlock - 1) / kBlock);
+    const int lpw = TPT_GEN_RES_LPW;
+    const int64_t per_block = (int64_t)(kBlock / 64) * lpw;
+    const unsigned gblocks = (unsigned)((count + per_block - 1) / per_block);
+    const auto gen_k = c->sc == 2 ? tpt_bdpt_gen_res_kernel<2> : c->sc == 1 ? tpt_bdpt_gen_res_kernel<1> : tpt_bdpt_gen_res_kernel<0>;
+    const WfState w0 = prep(c->wf[0], nb);
+    hipLaunchKernelGGL(gen_k, dim3(gblocks), dim3(kBlock), shmem, c->stream, c->ds, w0,
+                       ResArgs{wfi, nf, spp, c->wf_stride, rdone, rfree, camv, lpw});
+    const float inv = 1.0f / spp;
+    for (int f = 0, it0 = 0; f < nf; it0 += sched[f], ++f) {
+        const WfState w = prep(c->wf[f % kWfBufs], sched[f]);
+        hipLaunchKernelGGL(tpt_bdpt_wait_kernel, dim3(1), dim3(64), 0, s2, rdone + f, (unsigned)count, w.stall,
+                           c->stall_ticks);
+        const int rc = launch_wavefront_tail(c, s2, w, c->scan_tmp_g[0], it0, spp, inv, dsplat);
+        if (rc) return rc;
+        hipLaunchKernelGGL(tpt_bdpt_signal_kernel, dim3(1), dim3(64), 0, s2, rfree + f);
+    }
+    HIP_TRY(c, hipEventRecord(c->ev_fold[0], s2));
+    HIP_TRY(c, hipStreamWaitEvent(c->stream, c->ev_fold[0], 0));
+    hipLaunchKernelGGL(tpt_bdpt_out_kernel, dim3(pblocks), dim3(kBlock), 0, c->stream, w0, drows, dlist ? 1 : 0);
+    return TPT_OK;
+}
+
 // The BDPT sample loop over `count` (<= kWfChunk) pixel streams, as wavefronts of
 // nb = wf_iters(count, spp) sample iterations each.
 int launch_bdpt_chunk(tpt_ctx* c, int spp, int64_t begin, int64_t stride, int64_t count, const int64_t* dlist,
@@ -1195,6 +1661,16 @@ int launch_bdpt_chunk(tpt_ctx* c, int spp, int64_t begin, int64_t stride, int64_
     // gen(f + 2) only after fold(f).  Per pixel the order is kept: gen(f) samples after
     // gen(f - 1) (rngseq), fold is sequential on s2 (acc, splat).
     const int nb = (int)std::min<int64_t>(wf_iters(count, spp), std::max<int64_t>(1, c->wf_cap / count));
+    if (TPT_GEN_RES && !TPT_BDPT_SERIAL && !c->no_resident) {
+        int per_cu = 0;
+        const auto gk = c->sc == 2 ? tpt_bdpt_gen_res_kernel<2> : c->sc == 1 ? tpt_bdpt_gen_res_kernel<1> : tpt_bdpt_gen_res_kernel<0>;
+        HIP_TRY(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)gk, kBlock, shmem));
+        const int64_t lanes = (int64_t)std::max(per_cu, 1) * std::max(c->num_cu, 1) * kBlock * TPT_GEN_RES_LPW / 64;
+        if (count * 32 <= lanes * TPT_GEN_RES_Q) {
+            c->resident_used = true;
+            return launch_bdpt_resident(c, spp, begin, stride, count, dlist, drows, dsplat, nb);
+        }
+    }
     hipStream_t s2 = TPT_BDPT_SERIAL ? c->stream : c->stream2;
     // The second gen stream only where wavefronts hold several iterations (small
     // shards: a lane runs nb samples of one pixel, so gen's tail is long).  For a
@@ -1211,12 +1687,6 @@ int launch_bdpt_chunk(tpt_ctx* c, int spp, int64_t begin, int64_t stride, int64_
     HIP_TRY(c, hipStreamWaitEvent(s2, c->ev_start, 0));
     if (gs[1] != gs[0]) HIP_TRY(c, hipStreamWaitEvent(gs[1], c->ev_start, 0));
     const unsigned pblocks = (unsigned)((count + kBlock - 1) / kBlock);
-#ifndef TPT_CONN_GRID
-#define TPT_CONN_GRID 16384  // connect's grid-stride grid, small flat scenes (Standard BDPT 256 spp: 8192 / 16384 -> 445.4 / 441.2 ms)
-#endif
-#ifndef TPT_CONN_GRID_WALK
-#define TPT_CONN_GRID_WALK 8192  // ... and scenes with walk groups (bunny BDPT 256 spp: 8192 / 16384 -> 928 / 935 ms)
-#endif
     const int gen_q = c->sc != 2 ? TPT_GEN_GRID_Q
                       : !two_gen  ? TPT_GEN_GRID_Q_WALK
                       : nb >= 8   ? TPT_GEN_GRID_Q_WALK_SHARD
@@ -1241,21 +1711,24 @@ int launch_bdpt_chunk(tpt_ctx* c, int spp, int64_t begin, int64_t stride, int64_
         return fail(c, TPT_E_DEVICE, "BDPT: gen grid of " + std::to_string(gblocks) + " workgroups exceeds half of the " +
                                          std::to_string(resident) + " resident ones (two-stream hand-off invariant)");
     const float inv = 1.0f / spp;
-    for (int f = 0, it0 = 0; it0 < spp; ++f, it0 += nb) {
+    const std::vector<int> sched = wf_schedule(spp, nb);
+    int cam_nb[kWfBufs] = {};  // per buffer: leading iterations whose items hold the camera vertices
+    for (int f = 0, it0 = 0; it0 < spp; it0 += sched[f], ++f) {
         const int b = f % kWfBufs, gsi = f & 1;  // wavefront buffer, gen stream
         WfState w = c->wf[b];
         w.list = dlist;
         w.begin = begin;
         w.stride = stride;
         w.n = count;
-        w.nb = std::min(nb, spp - it0);
+        w.nb = sched[f];
         w.ni = (int64_t)w.nb * count;
+        w.cam_nb = cam_nb[b];
+        cam_nb[b] = std::max(cam_nb[b], w.nb);
         w.bounces = c->counters;
         w.stall = reinterpret_cast<int*>(c->counters + 4);
         w.stall_ticks = c->stall_ticks;
         w.drop_k = c->drop_k;
         w.conc = two_gen ? 1 : 0;
-        w.nbuf = kWfBufs;
         unsigned* queue = c->queue + b * 8 * 16;
         const unsigned iblocks = (unsigned)((w.ni + kBlock - 1) / kBlock);
         const unsigned cblocks = (unsigned)std::min<int64_t>(c->sc == 2 ? TPT_CONN_GRID_WALK : TPT_CONN_GRID,
@@ -1346,18 +1819,27 @@ int launch(tpt_ctx* c, int mode, int flags, int spp, int64_t begin, int64_t stri
         c->drop_k = dk && *dk ? std::atoi(dk) : -1;
         c->stall_ticks = dt && *dt ? (unsigned)std::strtoul(dt, nullptr, 10) : kStallTicks;
 #endif
+        c->resident_used = false;
         // Shards larger than kWfChunk pixel streams run as consecutive chunks.
         const int64_t chunk = std::min(count, kWfChunk), last = count - (count - 1) / kWfChunk * kWfChunk;
         if (dsplat) {
             const int rp = ensure_part(c);
             if (rp) return rp;
         }
-        int rc = ensure_wf(c, std::max(chunk * wf_iters(chunk, spp), last * wf_iters(last, spp)));
+        const int64_t want = std::max(chunk * wf_iters(chunk, spp), last * wf_iters(last, spp));
+        // a size that failed before for this shard size is not retried (each failed
+        // hipMalloc / hipFree pair synchronises the device): the fallback capacity stays
+        const bool known_bad = c->wf_failed && c->wf_failed_count == count && want >= c->wf_failed;
+        int rc = known_bad ? TPT_E_ALLOC : ensure_wf(c, want);
         if (rc) {
             // not enough device memory for multi-iteration wavefronts (~19 KB per item):
             // fall back to one iteration per wavefront (launch_bdpt_chunk caps nb at
             // wf_cap / count), which needs a shard's worth of items only
             (void)hipGetLastError();
+            if (!known_bad) {
+                c->wf_failed = want;
+                c->wf_failed_count = count;
+            }
             rc = ensure_wf(c, chunk);
             if (rc) return fail(c, TPT_E_ALLOC, "BDPT wavefront buffers: " + c->err);
         }
@@ -1390,6 +1872,11 @@ int launch(tpt_ctx* c, int mode, int flags, int spp, int64_t begin, int64_t stri
     if (mode == TPT_MODE_BDPT) {
         int stall = 0;
         HIP_TRY(c, hipMemcpy(&stall, c->counters + 4, sizeof(stall), hipMemcpyDeviceToHost));
+        if (stall && c->resident_used) {
+            c->no_resident = true;  // the streams did not run concurrently: use the queue design from now on
+            return fail(c, TPT_E_DEVICE, "BDPT: a resident gen lane or the connect stream timed out waiting for the "
+                                         "other (are the context's streams on distinct hardware queues?)");
+        }
         if (stall) return fail(c, TPT_E_DEVICE, "BDPT: a gen lane timed out waiting for the previous wavefront");
     }
     if (st) {
@@ -1426,6 +1913,27 @@ int check_render_args(tpt_ctx* c, int spp, int mode, int flags = 0) {
 extern "C" {
 
 int tpt_abi_version(void) { return TPT_ABI_VERSION; }
+void tpt_hip_versions(int* compiled, int* runtime) {
+    if (compiled) *compiled = HIP_VERSION;
+    int v = -1;
+    if (runtime && hipRuntimeGetVersion(&v) != hipSuccess) v = -1;
+    if (runtime) *runtime = v;
+}
+#if TPT_GEN_STATS
+// diagnostics build only: the gen kernels' per-wave statistics since the last reset
+int tpt_diag_genstats(unsigned long long* host, int64_t n, int reset) {
+    unsigned cnt = 0;
+    if (hipDeviceSynchronize() != hipSuccess || hipMemcpyFromSymbol(&cnt, HIP_SYMBOL(tpt_genstat_n), 4) != hipSuccess) return -1;
+    cnt = std::min<unsigned>(cnt, (unsigned)kGenStatMax);
+    const int64_t m = std::min<int64_t>(n, cnt);
+    if (m > 0 && hipMemcpyFromSymbol(host, HIP_SYMBOL(tpt_genstats), (size_t)m * 5 * 8) != hipSuccess) return -1;
+    if (reset) {
+        const unsigned z = 0;
+        if (hipMemcpyToSymbol(HIP_SYMBOL(tpt_genstat_n), &z, 4) != hipSuccess) return -1;
+    }
+    return (int)m;
+}
+#endif
 #if TPT_PT_WAVETIME
 // diagnostics build only: copy the PT kernel's per-wave (start, end, HW_ID) records
 int tpt_diag_wavetime(unsigned long long* host, int64_t n) {
@@ -1480,7 +1988,7 @@ void tpt_destroy(tpt_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (void* p : {(void*)c->blob, (void*)c->rgb, (void*)c->splat, (void*)c->splat_part, (void*)c->list, (void*)c->rows, (void*)c->counters,
-                    (void*)c->queue,
+                    (void*)c->queue, c->res_mem,
                     c->wf_mem, c->scan_tmp})
         if (p) (void)hipFree(p);
     if (c->stream2) (void)hipStreamSynchronize(c->stream2);

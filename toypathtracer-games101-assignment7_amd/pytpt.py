@@ -60,7 +60,8 @@ class Stats(ctypes.Structure):
 
 
 # Every symbol declared in include/tpt.h and include/tpt_host.h.
-EXPORTS = ("tpt_create", "tpt_destroy", "tpt_last_error", "tpt_abi_version", "tpt_upload_scene", "tpt_render",
+EXPORTS = ("tpt_create", "tpt_destroy", "tpt_last_error", "tpt_abi_version", "tpt_hip_versions",
+           "tpt_upload_scene", "tpt_render",
            "tpt_render_pixels", "tpt_render_device", "tpt_intersect", "tpt_camera_scale", "tpt_sample_seed",
            "tpt_multi_create", "tpt_multi_destroy", "tpt_multi_last_error", "tpt_multi_upload_scene",
            "tpt_render_multi",
@@ -117,6 +118,8 @@ def lib():
     L.tpt_render_multi.argtypes = [P, ctypes.POINTER(RenderParams), P, P, ctypes.POINTER(Stats)]
     if L.tpt_abi_version() != ABI_VERSION:  # Stats is ABI 2's layout (include/tpt.h)
         raise RuntimeError("%s has ABI %d, pytpt expects %d" % (LIB_PATH, L.tpt_abi_version(), ABI_VERSION))
+    L.tpt_hip_versions.argtypes = [ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]
+    L.tpt_hip_versions.restype = None
     _lib = L
     return L
 
@@ -151,6 +154,14 @@ class TptError(RuntimeError):
     pass
 
 
+def hip_versions():
+    """(HIP_VERSION libtpt was compiled against, the loaded runtime's; -1 if unknown).
+    Call after a context exists: reading the runtime's version initialises HIP."""
+    c, r = ctypes.c_int(0), ctypes.c_int(0)
+    lib().tpt_hip_versions(ctypes.byref(c), ctypes.byref(r))
+    return c.value, r.value
+
+
 class Context:
     """A libtpt context on one HIP device."""
 
@@ -161,6 +172,12 @@ class Context:
             raise TptError("tpt_create(%d) failed: %d" % (device, rc))
         self.h = h
         self.width = self.height = 0
+        self.hip_versions = hip_versions()
+        comp, run = self.hip_versions
+        if run >= 0 and run // 10000000 != comp // 10000000:
+            import warnings
+            warnings.warn("libtpt was compiled against HIP %d but runs on HIP runtime %d (another libamdhip64 "
+                          "was loaded first)" % (comp, run), RuntimeWarning)
 
     def _check(self, rc, what):
         if rc != TPT_OK:
@@ -234,6 +251,12 @@ class Multi:
             raise TptError("tpt_multi_create(%s) failed: %d" % (list(devs), rc))
         self.h = h
         self.width = self.height = 0
+        self.hip_versions = hip_versions()
+        comp, run = self.hip_versions
+        if run >= 0 and run // 10000000 != comp // 10000000:
+            import warnings
+            warnings.warn("libtpt was compiled against HIP %d but runs on HIP runtime %d (another libamdhip64 "
+                          "was loaded first)" % (comp, run), RuntimeWarning)
 
     def _check(self, rc, what):
         if rc != TPT_OK:
