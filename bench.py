@@ -191,6 +191,10 @@ def cpu_baseline(key, scene, mode, threads, info):
     return out
 
 
+ISA_CYCLES = {"ADD_F32": 2.0, "MUL_F32": 2.0, "FMA_F32": 2.0, "ADD_F64": 4.0, "MUL_F64": 4.0, "FMA_F64": 4.0,
+              "INT32": 2.0, "INT64": 4.0, "CVT": 2.0, "TRANS_F32": 8.0, "TRANS_F64": 16.0}
+
+
 def valu_roofline(key, kernel_ms, samples):
     """VALU-issue roofline of the workload's dominant kernel (see module docstring).
     `samples`: pixel-samples this rank's launch traced; the profiled issue cycles are
@@ -215,6 +219,14 @@ def valu_roofline(key, kernel_ms, samples):
             "note": "VALU issue cycles per launch (PMC class counts x measured cycles per wave-instruction, "
                     "profiles/valu_model.json) / live kernel time / (1,024 SIMDs x the profiled clock); "
                     "traffic = measured memory-side bytes per launch (profiles/traffic.json)"}
+    # the same class counts priced at the ISA's nominal issue rates instead of the measured
+    # table (full-rate 32-bit ops 2 cycles per wave64 instruction, 64-bit 4,
+    # quarter-rate transcendentals 8 / 16)
+    cls = model.get("class_insts_per_launch")
+    if cls:
+        isa = sum(n * ISA_CYCLES.get(c, 2.0) for c, n in cls.items()) + 2.0 * model.get("other_insts_per_launch", 0)
+        out["issue_cycles_per_launch_isa"] = round(isa * shard_frac)
+        out["frac_at_isa_rate"] = round(isa * shard_frac / (ms / 1e3) / 1e9 / peak, 4)
     if len(model.get("per_kernel", {})) > 1:  # BDPT: a sequence of kernels on two streams
         out["per_kernel_profiled"] = model["per_kernel"]
     return out
@@ -571,7 +583,8 @@ def summary(lines):
     for k, l in lines.items():
         rf, hm = l.get("roofline") or {}, l.get("roofline_hbm_measured") or {}
         out[k] = {"value": l["value"], "ms": l["ms_per_step"], "kernel_ms": l["kernel_ms_per_step"],
-                  "valu_frac": rf.get("frac"), "hbm_frac_measured": hm.get("frac"),
+                  "valu_frac": rf.get("frac"), "valu_frac_at_isa_rate": rf.get("frac_at_isa_rate"),
+                  "hbm_frac_measured": hm.get("frac"),
                   "cpu": (l.get("cpu_baseline") or {}).get("value")}
     return out
 

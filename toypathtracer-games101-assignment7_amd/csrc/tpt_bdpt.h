@@ -435,6 +435,14 @@ struct GenDefer {  // [slot][lane] in LDS
     TPT_D float& at(int slot) const { return base[slot * kBlock + threadIdx.x]; }
 };
 
+#ifndef TPT_GEN_STATS
+#define TPT_GEN_STATS 0
+#endif
+#if TPT_GEN_STATS
+// diagnostics only: [0] wave-ticks inside deferred-step walks, [1] such walks, [2] lanes
+// walking in them, [3] wave-ticks inside whole gen steps, [4] steps (100 MHz ticks)
+__device__ unsigned long long tpt_walkstat[8];
+#endif
 // One generation step (see the comment above gen_step's callers).  Returns 1 when the
 // subpath continues, 0 when it has ended (its vertex count is then i + 1), 2 when the
 // step was deferred (kDefer only; `pend` counts the iterations it has waited).
@@ -517,7 +525,27 @@ TPT_D int gen_step_t(const DScene& s, const WfState& w, int64_t k, int& phase, B
             pend = resumed ? pend + 1 : 1;
             return 2;
         }
+#if TPT_GEN_STATS
+        const unsigned long long tw0 = __builtin_amdgcn_s_memrealtime();
+        const unsigned long long wl = __ballot(need);
+        int wit = 0;
+        if (need) group_closest(s, gn, ray, cl, best, &wit);
+        int wmax = 0, wsum = 0;
+        for (unsigned long long m = wl; m; m &= m - 1) {
+            const int v = __builtin_amdgcn_readlane(wit, __builtin_ctzll(m));
+            wmax = max(wmax, v);
+            wsum += v;
+        }
+        if (wl && lane_id() == (unsigned)__builtin_ctzll(__ballot(true))) {
+            atomicAdd(&tpt_walkstat[0], __builtin_amdgcn_s_memrealtime() - tw0);
+            atomicAdd(&tpt_walkstat[1], 1ull);
+            atomicAdd(&tpt_walkstat[2], (unsigned long long)__popcll(wl));
+            atomicAdd(&tpt_walkstat[5], (unsigned long long)wsum);
+            atomicAdd(&tpt_walkstat[6], (unsigned long long)wmax);
+        }
+#else
         if (need) group_closest(s, gn, ray, cl, best);
+#endif
         pend = 0;
         closest_groups_c(s, gw + 1, s.ngroup, ray, cl, best);  // ... and after it
         it = ptv_bg();

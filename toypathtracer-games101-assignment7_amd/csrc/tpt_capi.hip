@@ -657,7 +657,17 @@ __global__ __launch_bounds__(kBlock, TPT_GEN_MINWAVES) void tpt_bdpt_gen_kernel(
         if (!run) continue;
         const int it = b * nn + k;
         int ln = -1;  // >= 0: the pixel's sample is complete
-        if (gen_step_t<kDef>(s, w, it, phase, prev, cur, i, rs, pend, dl, gw) == 0) {
+#if TPT_GEN_STATS
+        const unsigned long long ts0 = __builtin_amdgcn_s_memrealtime();
+#endif
+        const int gsr = gen_step_t<kDef>(s, w, it, phase, prev, cur, i, rs, pend, dl, gw);
+#if TPT_GEN_STATS
+        if (lane_id() == (unsigned)__builtin_ctzll(__ballot(true))) {
+            atomicAdd(&tpt_walkstat[3], __builtin_amdgcn_s_memrealtime() - ts0);
+            atomicAdd(&tpt_walkstat[4], 1ull);
+        }
+#endif
+        if (gsr == 0) {
             if (phase == 0) {
                 cn = i + 1;
                 phase = 1;
@@ -874,7 +884,17 @@ __global__ __launch_bounds__(kBlock, TPT_GEN_MINWAVES) void tpt_bdpt_gen_res_ker
         if (!run) continue;
         const int64_t ir = (int64_t)b * nn + k + boff_of(f);
         int ln = -1;
-        if (gen_step_t<kDef, !kWavePub>(s, w, ir, phase, prev, cur, i, rs, pend, dl, gw) == 0) {
+#if TPT_GEN_STATS
+        const unsigned long long ts0 = __builtin_amdgcn_s_memrealtime();
+#endif
+        const int gsr = gen_step_t<kDef, !kWavePub>(s, w, ir, phase, prev, cur, i, rs, pend, dl, gw);
+#if TPT_GEN_STATS
+        if (lane_id() == (unsigned)__builtin_ctzll(__ballot(true))) {
+            atomicAdd(&tpt_walkstat[3], __builtin_amdgcn_s_memrealtime() - ts0);
+            atomicAdd(&tpt_walkstat[4], 1ull);
+        }
+#endif
+        if (gsr == 0) {
             if (phase == 0) {
                 cn = i + 1;
                 phase = 1;
@@ -1921,6 +1941,14 @@ void tpt_hip_versions(int* compiled, int* runtime) {
 }
 #if TPT_GEN_STATS
 // diagnostics build only: the gen kernels' per-wave statistics since the last reset
+int tpt_diag_walkstats(unsigned long long* host, int reset) {
+    if (hipDeviceSynchronize() != hipSuccess || hipMemcpyFromSymbol(host, HIP_SYMBOL(tpt_walkstat), 64) != hipSuccess) return -1;
+    if (reset) {
+        const unsigned long long z[8] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(tpt_walkstat), z, 64) != hipSuccess) return -1;
+    }
+    return 0;
+}
 int tpt_diag_genstats(unsigned long long* host, int64_t n, int reset) {
     unsigned cnt = 0;
     if (hipDeviceSynchronize() != hipSuccess || hipMemcpyFromSymbol(&cnt, HIP_SYMBOL(tpt_genstat_n), 4) != hipSuccess) return -1;

@@ -326,11 +326,12 @@ TPT_D DTri load_gtri(const DTri* p) {
     return t;
 }
 template <bool kShadow>
-TPT_D bool walk4(const DScene& s, int q, const Ray& r, int cull, Hit& best, V3 lc, double thr) {
+TPT_D bool walk4(const DScene& s, int q, const Ray& r, int cull, Hit& best, V3 lc, double thr, int* iters = nullptr) {
     uint16_t* st = s.ws + threadIdx.x;  // [slot][lane]
     int sp = 0;
     int cur = q;
     for (;;) {
+        if (iters) ++*iters;
         // a leaf: its triangle test (BVHAccel::Intersect's strict `>` fold, or the
         // shadow answer), then the next entry -- in the same step, so a lane does one
         // triangle and one QNode per step and the two kinds of work do not alternate
@@ -372,11 +373,12 @@ TPT_D bool walk4(const DScene& s, int q, const Ray& r, int cull, Hit& best, V3 l
 }
 // A walk group's closest hit / shadow answer: the 4-wide walk where the group has a
 // 4-wide tree and the kernel gave its lanes stacks, else the threaded binary walk.
+// (`iters`: diagnostics builds count the lane's walk steps.)
 #ifndef TPT_WALK4
 #define TPT_WALK4 1
 #endif
-TPT_D void group_closest(const DScene& s, const DNode& gn, const Ray& r, int cull, Hit& best) {
-    if (TPT_WALK4 && gn.b <= -2 && s.ws) walk4<false>(s, -2 - gn.b, r, cull, best, r.o, 0.0);
+TPT_D void group_closest(const DScene& s, const DNode& gn, const Ray& r, int cull, Hit& best, int* iters = nullptr) {
+    if (TPT_WALK4 && gn.b <= -2 && s.ws) walk4<false>(s, -2 - gn.b, r, cull, best, r.o, 0.0, iters);
     else walk_group_closest(s, gn.a, r, cull, best);
 }
 TPT_D bool group_shadow(const DScene& s, const DNode& gn, const Ray& r, V3 lc, double thr, int cull) {
