@@ -173,6 +173,9 @@ static_assert(kQ == 1 || kQ == 2 || kQ == 4 || kQ == 8 || kQ == 16, "Q must be a
                              // unchanged)
 #endif
 
+#ifndef TPT_PT_CONE
+#define TPT_PT_CONE 1  // PT's shadow queries skip the leaves outside the wave's shadow cone (pt_cone_mask)
+#endif
 #ifndef TPT_PT_DPP
 #define TPT_PT_DPP 1
 #endif
@@ -221,6 +224,19 @@ TPT_D void pt_tier(const DScene& s, unsigned char* lds_free, const uint32_t* jt,
         const V3 dir = pixel_ray(px, py, s.width, s.height, s.scale);
         const Ray r = make_ray(v3(s.eye[0], s.eye[1], s.eye[2]), dir);
         PTV v = scene_intersect(s, r, TPT_CULL_BACK);
+        // the wave's shadow-cone mask (pt_cone_mask): the OR of its pixels' masks, with
+        // every lane of the wave here; wave-uniform (SGPRs) across the sample loop
+        uint64_t cone = ~0ull;
+        if (TPT_PT_CONE && (s.flat & kFlatShadow) && s.nleaf <= 64 && s.n_emitters > 0) {
+            const uint64_t cm = on && v.type != T_BG ? pt_cone_mask(s, v.x) : 0ull;
+            uint32_t lo = (uint32_t)cm, hi = (uint32_t)(cm >> 32);
+            for (int o = 1; o < 64; o <<= 1) {
+                lo |= (uint32_t)__shfl_xor((int)lo, o);
+                hi |= (uint32_t)__shfl_xor((int)hi, o);
+            }
+            cone = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)lo) |
+                   (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)hi) << 32;
+        }
         if (on && v.type != T_BG) {
             const int mi = prim_mat(s, v.prim);
             const Mat m = load_mat(s, mi);
@@ -243,7 +259,7 @@ TPT_D void pt_tier(const DScene& s, unsigned char* lds_free, const uint32_t* jt,
                         const int64_t kk = k0 + (blk * kBlock + ln) / kQP;
                         rs = sample_seed(list ? list[kk] : begin + kk * stride, j0 + qq);
                     }
-                    L = mul(pt_sample(s, px, rs), inv);
+                    L = mul(pt_sample(s, px, rs, cone), inv);
                     if (kQP > 1 && !kSeeded) {
                         const int ty = px.type(s);
                         rs = kQP > 2 && use_jump && ty != TPT_METAL
@@ -2115,6 +2131,8 @@ int tpt_upload_scene(tpt_ctx* c, const tpt_scene_desc* d) {
     ds.width = hs.width;
     ds.height = hs.height;
     ds.scale = camera_scale(hs.fov);
+    for (int k = 0; k < 6; ++k) ds.lbox[k] = hs.lbox[k];
+    ds.cone_delta = hs.cone_delta;
     for (int k = 0; k < 3; ++k) { ds.eye[k] = hs.eye[k]; ds.bg[k] = hs.bg[k]; }
     ds.lds_bytes = (int)lds_b;
     // flat (all-leaves) queries for small scenes; TPT_FLAT overrides the bits: 0 walks

@@ -420,10 +420,16 @@ TPT_D Hit traverse_flat(const DScene& s, const Ray& r, int cull) {
     return best;
 }
 // Any hit with |hit - lc|^2 < thr over all leaves (see shadow_pts for why any-hit is exact).
-TPT_D bool shadow_flat(const DScene& s, const Ray& r, V3 lc, double thr, int cull) {
+// `wm` (wave-uniform): the flat leaves that can hold a counting hit for every active
+// lane's query (PT's shadow-cone mask, pt_cone_mask); the others are skipped untested.
+TPT_D bool shadow_flat(const DScene& s, const Ray& r, V3 lc, double thr, int cull, uint64_t wm = ~0ull) {
     bool sh = false;
     for (int gi = 0; gi < s.ngroup; ++gi) {
         const DNode gn = s.groups[gi];
+        if (!(s.big && gn.b < 0)) {  // a flat group: skip it whole when none of its leaves is a candidate
+            const uint64_t gbits = (gn.b >= 64 ? ~0ull : (1ull << gn.b) - 1) << gn.a;
+            if ((wm & gbits) == 0) continue;
+        }
         const bool pass =
             !sh && slab_hit_finite(gn.bmin[0], gn.bmin[1], gn.bmin[2], gn.bmax[0], gn.bmax[1], gn.bmax[2], r);
         if (__ballot(pass) == 0) continue;
@@ -433,6 +439,7 @@ TPT_D bool shadow_flat(const DScene& s, const Ray& r, V3 lc, double thr, int cul
         }
         const int j1 = gn.a + gn.b;
         for (int j = gn.a; j < j1; ++j) {
+            if (!((wm >> j) & 1)) continue;
             const DNode n = s.leaves[j];
             if (!sh && slab_hit_finite(n.bmin[0], n.bmin[1], n.bmin[2], n.bmax[0], n.bmax[1], n.bmax[2], r)) {
                 const int prim = -1 - n.a;
@@ -799,14 +806,69 @@ TPT_D bool shadow_walk(const DScene& s, const Ray& r, V3 lc, double thr, int cul
 }
 // The shadow query of Scene::ShadowCheck from lc toward x: flat all-leaves query
 // when every ray of the wave has a finite inv, else a per-lane threaded walk.
-TPT_D bool shadow_ray(const DScene& s, V3 lc, V3 x, int cull) {
+// `cone` (PT only): the wave's shadow-cone mask for queries from an emitter point toward
+// the lanes' camera hits (pt_cone_mask); used when every active lane's origin lies on
+// the emitters (their box grown by half the margin), else every leaf is a candidate.
+TPT_D bool shadow_ray(const DScene& s, V3 lc, V3 x, int cull, uint64_t cone = ~0ull) {
     const double ld2 = dot3(lc - x, lc - x);
     const double thr = ld2 - 1.0f;
     if (!(thr > 0.0)) return false;  // d2 >= 0 can never be < thr (the lane leaves the wave's query)
     const Ray r = make_ray(lc, normalized(x - lc));
     const bool fin = wave_finite(r);
-    if (fin && (s.flat & kFlatShadow)) return s.qs ? shadow_flat_c(s, r, thr, cull) : shadow_flat(s, r, lc, thr, cull);
+    if (fin && (s.flat & kFlatShadow)) {
+        if (s.qs) return shadow_flat_c(s, r, thr, cull);
+        if (cone != ~0ull) {
+            const float h = 0.5f * s.cone_delta;
+            const bool on_e = lc.x >= s.lbox[0] - h && lc.y >= s.lbox[1] - h && lc.z >= s.lbox[2] - h &&
+                              lc.x <= s.lbox[3] + h && lc.y <= s.lbox[4] + h && lc.z <= s.lbox[5] + h;
+            if (__ballot(!on_e) != 0) cone = ~0ull;  // e.g. the light branch's query from (0,0,0)
+        }
+        return shadow_flat(s, r, lc, thr, cull, cone);
+    }
     return fin ? shadow_walk<true>(s, r, lc, thr, cull) : shadow_walk<false>(s, r, lc, thr, cull);
+}
+
+// PT shadow-cone mask (round 5).  Both of PathTrace's shadow queries run from a point on
+// an emitter (the light sample's re-intersection, or the BSDF ray's hit on the light) to
+// the pixel's camera hit x, which is the same for all its samples.  A hit that counts
+// (|hit - lc|^2 < |x - lc|^2 - 1, Scene.cpp:37-48) lies on that segment, so inside
+// H = conv(E u {x}), E the emitters' box; its primitive lies in its leaf box, so a leaf
+// whose box cannot meet H (both grown by cone_delta, which covers the rounding of the
+// origin, the direction, the hit point and Moller-Trumbore's float edges) holds no
+// counting hit and may be skipped: the any-hit answer is unchanged.  H is exactly the
+// union over s in [0, 1] of the boxes x + s (E - x), so a leaf box L meets it iff the
+// per-axis conditions  x + s (Emin - x) <= Lmax,  x + s (Emax - x) >= Lmin  have a common
+// s in [0, 1]: six linear bounds on s per leaf.  Bit j: flat leaf j is a candidate.
+TPT_D uint64_t pt_cone_mask(const DScene& s, V3 x) {
+    const float dl = s.cone_delta;
+    const float xv[3] = {x.x, x.y, x.z};
+    float c1[3], c2[3], i1[3], i2[3];
+    for (int a = 0; a < 3; ++a) {
+        c1[a] = (s.lbox[a] - dl) - xv[a];
+        c2[a] = (s.lbox[3 + a] + dl) - xv[a];
+        i1[a] = __builtin_amdgcn_rcpf(c1[a]);
+        i2[a] = __builtin_amdgcn_rcpf(c2[a]);
+    }
+    uint64_t m = 0;
+    for (int j = 0; j < s.nleaf && j < 64; ++j) {
+        const DNode n = s.leaves[j];
+        float lo = 0.0f, hi = 1.0f;
+        bool ok = true;
+        for (int a = 0; a < 3; ++a) {
+            const float r1 = (n.bmax[a] + dl) - xv[a];  // c1 s <= r1
+            const float r2 = (n.bmin[a] - dl) - xv[a];  // c2 s >= r2
+            if (c1[a] > 0.0f) hi = fminf(hi, r1 * i1[a]);
+            else if (c1[a] < 0.0f) lo = fmaxf(lo, r1 * i1[a]);
+            else ok = ok && r1 >= 0.0f;
+            if (c2[a] > 0.0f) lo = fmaxf(lo, r2 * i2[a]);
+            else if (c2[a] < 0.0f) hi = fminf(hi, r2 * i2[a]);
+            else ok = ok && r2 <= 0.0f;
+        }
+        // the bounds are quotients rounded a few ulps either way: a relative slack keeps
+        // the test conservative (the margins above are far larger)
+        if (ok && lo <= hi + 1e-5f * (1.0f + fabs_(hi))) m |= 1ull << j;
+    }
+    return m;
 }
 
 // ------------------------------------------------------------ materials --
@@ -1352,7 +1414,7 @@ TPT_D V3 opaque(V3 a) {
     asm volatile("" : "+v"(a.x), "+v"(a.y), "+v"(a.z));
     return a;
 }
-TPT_D V3 pt_sample(const DScene& s, PixPark px, uint32_t& rs) {
+TPT_D V3 pt_sample(const DScene& s, PixPark px, uint32_t& rs, uint64_t cone = ~0ull) {
     V3 result = v3s(0.0f);
     {
         const DMat& dm = s.mats[px.mat_index()];
@@ -1396,7 +1458,7 @@ TPT_D V3 pt_sample(const DScene& s, PixPark px, uint32_t& rs) {
                 if (hb.prim >= 0) {
                     V3 hx, hn;
                     hit_geometry(s, rb, hb, hx, hn);
-                    const bool sh = shadow_ray(s, hx, px.v(kPxX), TPT_CULL_BACK);
+                    const bool sh = shadow_ray(s, hx, px.v(kPxX), TPT_CULL_BACK, cone);
                     if (!sh)
                         ev = ev + divs(eval_bsdf(px.mat(s), px.v(kPxWo), opaque(wib), px.shade(), true),
                                        1e-4f + pdf_b + pbl);
@@ -1416,7 +1478,7 @@ TPT_D V3 pt_sample(const DScene& s, PixPark px, uint32_t& rs) {
             Hit hl = object_hit(s, o, rl, TPT_CULL_BACK);
             V3 hx = v3s(0.0f), hn;  // default Intersection::coords when missed (Intersection.hpp:14-21)
             if (hl.prim >= 0) hit_geometry(s, rl, hl, hx, hn);
-            const bool sh = shadow_ray(s, hx, px.v(kPxX), TPT_CULL_BACK);
+            const bool sh = shadow_ray(s, hx, px.v(kPxX), TPT_CULL_BACK, cone);
             if (!sh) ev = ev + divs(fl, 1e-4f + pll + plb);
         }
         result = result + ev * load_mat(s, o.mat).em;

@@ -146,6 +146,8 @@ struct DScene {
     int32_t width;
     int32_t height;
     float scale;  // CalculateScale(fov) (SceneRenderingHelper.cpp:12-14), host-computed
+    float lbox[6];     // the emitters' bounding box (min xyz, max xyz): PT shadow-cone masks
+    float cone_delta;  // ... and their margin (HostScene::cone_delta)
     float eye[3];
     float bg[3];
     int32_t nmats;

@@ -480,6 +480,41 @@ int build_host_scene(const tpt_scene_desc* d, HostScene& hs, std::string& err) {
     hs.height = d->height;
     for (int k = 0; k < 3; ++k) { hs.eye[k] = d->eye[k]; hs.bg[k] = d->background[k]; }
     hs.fov = d->fov;
+    // PT shadow-cone masks (pt_cone_mask, tpt_device.h): the emitters' box and the margin
+    double cmax = 0.0;
+    for (int k = 0; k < 3; ++k) cmax = std::max(cmax, (double)std::fabs(hs.eye[k]));
+    for (size_t t = 0; t < hs.tris.size(); ++t)
+        for (int k = 0; k < 3; ++k)
+            cmax = std::max({cmax, (double)std::fabs(hs.tris[t].v0[k]), (double)std::fabs(hs.trix[t].v1[k]),
+                             (double)std::fabs(hs.trix[t].v2[k])});
+    for (const DSphere& sp : hs.sph)
+        for (int k = 0; k < 3; ++k) cmax = std::max(cmax, (double)std::fabs(sp.c[k]) + std::fabs(sp.r));
+    hs.cone_delta = (float)std::max(cmax * 0x1p-12, 0x1p-60);
+    float lb[6] = {std::numeric_limits<float>::max(), std::numeric_limits<float>::max(),
+                   std::numeric_limits<float>::max(), -std::numeric_limits<float>::max(),
+                   -std::numeric_limits<float>::max(), -std::numeric_limits<float>::max()};
+    auto grow = [&](const float* p) {
+        for (int k = 0; k < 3; ++k) {
+            lb[k] = std::min(lb[k], p[k]);
+            lb[3 + k] = std::max(lb[3 + k], p[k]);
+        }
+    };
+    for (int o : hs.emitters) {
+        if (d->objects[o].kind == TPT_OBJ_MESH) {
+            for (int t = mesh_tris[o].first; t < mesh_tris[o].first + mesh_tris[o].count; ++t) {
+                grow(hs.tris[t].v0);
+                grow(hs.trix[t].v1);
+                grow(hs.trix[t].v2);
+            }
+        } else {
+            const DSphere& sp = hs.sph[sphere_prim[o] - ntri];
+            const float lo[3] = {sp.c[0] - sp.r, sp.c[1] - sp.r, sp.c[2] - sp.r};
+            const float hi[3] = {sp.c[0] + sp.r, sp.c[1] + sp.r, sp.c[2] + sp.r};
+            grow(lo);
+            grow(hi);
+        }
+    }
+    for (int k = 0; k < 6; ++k) hs.lbox[k] = lb[k];
     return TPT_OK;
 }
 

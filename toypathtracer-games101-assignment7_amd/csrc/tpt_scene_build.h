@@ -23,6 +23,11 @@ struct HostScene {
     std::vector<DMat> mats;
     std::vector<DObj> objs;
     std::vector<int32_t> emitters;
+    // the emitters' bounding box (every emitter's triangle vertices and sphere bounds) and
+    // the margin of the PT shadow-cone masks (pt_cone_mask): C * 2^-12, C bounding every
+    // scene and eye coordinate
+    float lbox[6] = {0, 0, 0, 0, 0, 0};
+    float cone_delta = 0.0f;
     int width = 0, height = 0;
     float eye[3] = {0, 0, 0};
     float bg[3] = {0, 0, 0};
