@@ -542,7 +542,7 @@ class Runner:
             line["kernel_ms_max_over_ranks"] = max(r["kernel_ms"] for r in ranks)
         return line
 
-    def shard_model(self):
+    def shard_model(self, c5_line=None):
         """The N-way pixel split of configs 2, 3 and 5 modelled on this one GPU: every
         stride-N shard is rendered alone (tpt_render_device, as rank r of an N-GPU run
         renders it) and timed with the library's HIP events (sharding.shard_model)."""
@@ -569,6 +569,22 @@ class Runner:
                                                   "" if spp == WORKLOADS[key][2] else
                                                   " (configs[4] at a reduced spp: same per-iteration chain)")
             out[key] = res
+        if c5_line is not None:
+            # configs[4] at its own 4096 spp, split 8 ways (the run BASELINE defines it on):
+            # every 1/8 shard against the c5 line's whole frame (same process, same scene)
+            scene, mode, spp = WORKLOADS["c5"]
+            if self.scene != scene:
+                self.ctx.upload(pytpt.Preset(scene))
+                self.scene = scene
+            fb = self.fb
+
+            def render8(begin, stride):
+                st = self.ctx.render_device(spp, pytpt.MODE_BDPT, fb[0].data_ptr(), fb[1].data_ptr(), begin, stride, 0)
+                return st.kernel_ms, st.total_ms
+
+            res = self.sharding.shard_model(render8, (8,), full=(c5_line["kernel_ms_per_step"], c5_line["ms_per_step"]))
+            res["workload"] = "bunny BDPT 4096 spp (configs[4] itself); whole frame = the c5 line's"
+            out["c5_4096"] = res
         return out
     
     def close(self):
@@ -613,7 +629,7 @@ def main():
     for k in keys:
         steps, warmup = (a.steps, a.warmup) if k == keys[0] else SUB_STEPS[k]
         lines[k] = r.run(k, steps, warmup)
-    shard_model = r.shard_model() if (a.mode is None and r.world == 1 and not a.no_shard_model) else None
+    shard_model = r.shard_model(lines.get("c5")) if (a.mode is None and r.world == 1 and not a.no_shard_model) else None
     if r.rank == 0:
         if want_cpu:
             for k in keys:
@@ -638,6 +654,9 @@ def main():
         if shard_model is not None:
             out["shard_model"] = shard_model
         out["summary"] = summary(lines)
+        if shard_model is not None:  # the one-GPU model's efficiencies (kernel time), N = 2 / 4 / 8
+            out["summary"]["shard_eff"] = {k: [v["n%d" % n]["eff_kernel"] for n in SHARD_NS if "n%d" % n in v]
+                                           for k, v in shard_model.items() if isinstance(v, dict)}
         bad = check_distinct(out, r.world)
         if bad:
             out["distinct_devices_error"] = bad

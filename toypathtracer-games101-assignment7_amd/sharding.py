@@ -35,7 +35,7 @@ def reduce_frame(dist, fb, dst=0):
     return fb
 
 
-def shard_model(render, ns=(2, 4, 8)):
+def shard_model(render, ns=(2, 4, 8), full=None):
     """One-GPU model of the N-way split.  `render(begin, stride)` renders one shard
     alone and returns (kernel_ms, wall_ms).  For each N every shard r = 0..N-1 is
     rendered in turn (the frame rank r of an N-GPU run would render); the model is
@@ -45,8 +45,9 @@ def shard_model(render, ns=(2, 4, 8)):
     with T_1 the whole frame's time: eff_N = 1 when the split costs nothing (the work
     divides evenly and no per-launch cost fails to shrink).  Both the device time
     (HIP events around the kernels) and the wall time of the synchronous call are
-    reported; the reduce is not part of the model."""
-    k1, w1 = render(0, 1)
+    reported; the reduce is not part of the model.  `full`: the whole frame's (kernel_ms,
+    wall_ms) when the caller has just measured it."""
+    k1, w1 = full if full is not None else render(0, 1)
     out = {"full_kernel_ms": round(k1, 3), "full_wall_ms": round(w1, 3)}
     for n in ns:
         ks, ws = zip(*[render(r, n) for r in range(n)])
