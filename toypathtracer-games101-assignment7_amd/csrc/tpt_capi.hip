@@ -1571,7 +1571,8 @@ std::vector<int> wf_schedule(int spp, int nb) {
 #define TPT_CONN_GRID 16384  // connect's grid-stride grid, small flat scenes (Standard BDPT 256 spp: 8192 / 16384 -> 445.4 / 441.2 ms)
 #endif
 #ifndef TPT_CONN_GRID_WALK
-#define TPT_CONN_GRID_WALK 8192  // ... and scenes with walk groups (bunny BDPT 256 spp: 8192 / 16384 -> 928 / 935 ms)
+#define TPT_CONN_GRID_WALK 16384  // ... and scenes with walk groups (round 3, bunny BDPT 256 spp: 8192 / 16384 -> 928 / 935 ms;
+                                  // round 5, with the partition: 716.3 / 715.5 ms, its 1/8 shard at 4096 spp 1597 / 1577 ms)
 #endif
 
 // The per-wavefront chain on the connect stream s2: scan, scatter, connect, strategy sums
