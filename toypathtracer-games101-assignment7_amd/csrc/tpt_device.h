@@ -807,9 +807,9 @@ TPT_D bool shadow_walk(const DScene& s, const Ray& r, V3 lc, double thr, int cul
 // The shadow query of Scene::ShadowCheck from lc toward x: flat all-leaves query
 // when every ray of the wave has a finite inv, else a per-lane threaded walk.
 // `cone` (PT only): the wave's shadow-cone mask for queries from an emitter point toward
-// the lanes' camera hits (pt_cone_mask); used when every active lane's origin lies on
-// the emitters (their box grown by half the margin), else every leaf is a candidate.
-TPT_D bool shadow_ray(const DScene& s, V3 lc, V3 x, int cull, uint64_t cone = ~0ull) {
+// the lanes' camera hits (pt_cone_mask); used when every active lane's origin is a hit on
+// an emitter (`on_e`), else every leaf is a candidate.
+TPT_D bool shadow_ray(const DScene& s, V3 lc, V3 x, int cull, uint64_t cone = ~0ull, bool on_e = false) {
     const double ld2 = dot3(lc - x, lc - x);
     const double thr = ld2 - 1.0f;
     if (!(thr > 0.0)) return false;  // d2 >= 0 can never be < thr (the lane leaves the wave's query)
@@ -817,19 +817,15 @@ TPT_D bool shadow_ray(const DScene& s, V3 lc, V3 x, int cull, uint64_t cone = ~0
     const bool fin = wave_finite(r);
     if (fin && (s.flat & kFlatShadow)) {
         if (s.qs) return shadow_flat_c(s, r, thr, cull);
-        if (cone != ~0ull) {
-            const float h = 0.5f * s.cone_delta;
-            const bool on_e = lc.x >= s.lbox[0] - h && lc.y >= s.lbox[1] - h && lc.z >= s.lbox[2] - h &&
-                              lc.x <= s.lbox[3] + h && lc.y <= s.lbox[4] + h && lc.z <= s.lbox[5] + h;
-            if (__ballot(!on_e) != 0) cone = ~0ull;  // e.g. the light branch's query from (0,0,0)
-        }
+        if (cone != ~0ull && __ballot(!on_e) != 0) cone = ~0ull;  // e.g. the light branch's query from (0,0,0)
         return shadow_flat(s, r, lc, thr, cull, cone);
     }
     return fin ? shadow_walk<true>(s, r, lc, thr, cull) : shadow_walk<false>(s, r, lc, thr, cull);
 }
 
 // PT shadow-cone mask (round 5).  Both of PathTrace's shadow queries run from a point on
-// an emitter (the light sample's re-intersection, or the BSDF ray's hit on the light) to
+// an emitter (the light sample's re-intersection, or the BSDF ray's hit on the light --
+// hit points computed within a few ulps of the emitter's triangles or sphere) to
 // the pixel's camera hit x, which is the same for all its samples.  A hit that counts
 // (|hit - lc|^2 < |x - lc|^2 - 1, Scene.cpp:37-48) lies on that segment, so inside
 // H = conv(E u {x}), E the emitters' box; its primitive lies in its leaf box, so a leaf
@@ -1458,7 +1454,7 @@ TPT_D V3 pt_sample(const DScene& s, PixPark px, uint32_t& rs, uint64_t cone = ~0
                 if (hb.prim >= 0) {
                     V3 hx, hn;
                     hit_geometry(s, rb, hb, hx, hn);
-                    const bool sh = shadow_ray(s, hx, px.v(kPxX), TPT_CULL_BACK, cone);
+                    const bool sh = shadow_ray(s, hx, px.v(kPxX), TPT_CULL_BACK, cone, true);  // hx: a hit on the emitter
                     if (!sh)
                         ev = ev + divs(eval_bsdf(px.mat(s), px.v(kPxWo), opaque(wib), px.shade(), true),
                                        1e-4f + pdf_b + pbl);
@@ -1478,7 +1474,7 @@ TPT_D V3 pt_sample(const DScene& s, PixPark px, uint32_t& rs, uint64_t cone = ~0
             Hit hl = object_hit(s, o, rl, TPT_CULL_BACK);
             V3 hx = v3s(0.0f), hn;  // default Intersection::coords when missed (Intersection.hpp:14-21)
             if (hl.prim >= 0) hit_geometry(s, rl, hl, hx, hn);
-            const bool sh = shadow_ray(s, hx, px.v(kPxX), TPT_CULL_BACK, cone);
+            const bool sh = shadow_ray(s, hx, px.v(kPxX), TPT_CULL_BACK, cone, hl.prim >= 0);
             if (!sh) ev = ev + divs(fl, 1e-4f + pll + plb);
         }
         result = result + ev * load_mat(s, o.mat).em;
