@@ -486,7 +486,7 @@ TPT_D int gen_step_t(const DScene& s, const WfState& w, int64_t k, int& phase, B
         if (go) {
             const V3 wo = normalized(prev.x - cur.x);
             float raw;
-            const V3 wi = mat_sample(load_mat(s, cur.mat), wo, cur.N, &raw, rs);
+            const V3 wi = mat_sample<true>(load_mat(s, cur.mat), wo, cur.N, &raw, rs);  // same draws, fewer live values
             const float rr = i > 4 ? .8f : 1.f;
             go = !(rng_float(rs) > rr);
             if (go) {
