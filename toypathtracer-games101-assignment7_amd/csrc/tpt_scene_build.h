@@ -24,7 +24,7 @@ struct HostScene {
     std::vector<DObj> objs;
     std::vector<int32_t> emitters;
     // the emitters' bounding box (every emitter's triangle vertices and sphere bounds) and
-    // the margin of the PT shadow-cone masks (pt_cone_mask): C * 2^-12, C bounding every
+    // the margin of the PT shadow-cone masks (pt_cone_mask): C * 2^-16, C bounding every
     // scene and eye coordinate
     float lbox[6] = {0, 0, 0, 0, 0, 0};
     float cone_delta = 0.0f;
