@@ -68,6 +68,11 @@ def test_bdpt_frame(ctx, cfg):
     what = "%s BDPT %d spp" % (g["preset"], g["spp"])
     check_exact(rgb, g, "rgb", what + " radiance")
     assert st.nonfinite == len(g["rgb_nonfinite"])
+    # every strategy is clamped at 0 (BDPT.cpp:306): non-negative radiance and splats
+    # (configs[4]'s frame also holds the reference's own NaN pixel 485594, pinned above)
+    rows = rgb.reshape(-1, 3)
+    fin = np.isfinite(rows).all(1)
+    assert rows[fin].min() >= 0 and np.nanmin(splat) >= 0 and np.nansum(splat) > 0
     # the device count of non-finite splat pixels agrees with the buffer; where they
     # may sit is check_close's (non-finite blocks must be the reference's)
     assert st.nonfinite_splat == int((~np.isfinite(splat.reshape(-1, 3)).all(1)).sum())
