@@ -435,6 +435,146 @@ struct GenDefer {  // [slot][lane] in LDS
     TPT_D float& at(int slot) const { return base[slot * kBlock + threadIdx.x]; }
 };
 
+// Deferred walks with work stealing (round 5, TPT_WALK_STEAL).  A wave's deferred walk
+// ran as long as its longest lane's (46 steps against 16.9 on average, ~20 of 64 lanes
+// walking): the other lanes idled.  Here every lane of the wave that reached the walk
+// takes part.  A lane whose walk has ended (or that had none) takes the bottom entry
+// of another lane's pending stack -- a whole subtree of that lane's ray -- and walks it
+// with the owner's ray (rebuilt from the owner's LDS slots: the same make_ray, so the
+// same bits).  Each job (a subtree) folds its triangles in its own DFS order with
+// BVHAccel::Intersect's strict `>` (BVH.cpp:103-143), which keeps the job's nearest hit
+// of smallest DFS rank; the jobs' hits are then merged per ray by (distance, DFS rank)
+// (HostScene::grank), which is exactly the sequential fold's answer: its first
+// minimum.  (The merge is a wave-uniform scan of the list by each owner; a version
+// with LDS atomic minima lost hits and was not kept.)  The walk group's leaves all follow the flat groups before it in the DFS
+// order and precede the ones after, so the caller folds the merged hit into `best`
+// with the same strict `>`.  Distances are finite (finite rays, |det| >= 1e-4), and
+// -0.0 ties +0.0 as in the reference (the key clears the sign; the winner's own bits
+// are returned).  Only the time differs from the per-lane walk.
+#ifndef TPT_WALK_STEAL
+#define TPT_WALK_STEAL 1
+#endif
+// the origin's slots while a walk runs (their parked values are in registers by then)
+enum { kGdOx = kGdPrim, kGdOy = kGdDlo, kGdOz = kGdDhi };
+constexpr int kStealList = kQC - 64;  // QScratch::res[kStealList, kQC) holds the rays' minima
+TPT_D unsigned long long dist_key(double d) { return (unsigned long long)__double_as_longlong(d) & 0x7fffffffffffffffull; }
+TPT_D Ray owner_ray(const GenDefer& dl, int l, int& cl) {
+    const float* b = dl.base + ((int)threadIdx.x & ~63) + l;
+    cl = __float_as_int(b[kGdCl * kBlock]);
+    return make_ray(v3(b[kGdOx * kBlock], b[kGdOy * kBlock], b[kGdOz * kBlock]),
+                    v3(b[kGdDx * kBlock], b[kGdDy * kBlock], b[kGdDz * kBlock]));
+}
+// `need` lanes walk the group whose 4-wide root is qnodes[root] with their ray (r, cl),
+// which they have stored in their dl slots; returns each need lane's first-minimum hit
+// in the group (prim -1: none).  Every active lane must call it (wave-synchronous).
+TPT_D Hit walk4_steal(const DScene& s, int root, bool need, Ray r, int cl, const GenDefer& dl) {
+    QScratch* qs = wave_qs(s);
+    const int lane = (int)__lane_id();
+    uint16_t* st = s.ws + threadIdx.x;  // [slot][lane]
+    int sb = 0, sp = 0, cur = root, owner = lane;
+    bool job = need;
+    Hit jb;
+    jb.prim = -1;
+    jb.dist = 0.0;
+    int ncnt = 0, jobs = __popcll(__ballot(need));
+    for (;;) {
+        bool done = false;
+        if (job) {  // one step of the job's walk (walk4's)
+            if (cur < 0) {
+                const int prim = -1 - cur;
+                double dist;
+                if (tri_test(load_gtri(s.gtris + prim), r, cl, dist) && (jb.prim < 0 || jb.dist > dist)) {
+                    jb.dist = dist;
+                    jb.prim = prim;
+                }
+                if (sp == sb) done = true;
+                else cur = (int)(int16_t)st[kBlock * --sp];
+            }
+            if (!done && cur >= 0) {
+                const QNode4 n = load_qnode(s.qnodes + cur);
+                int held = kQNone;
+                for (int j = kWalkW - 1; j >= 0; --j) {
+                    const bool pass = n.e[j] != kQNone && slab_hit_finite(n.bmin[0][j], n.bmin[1][j], n.bmin[2][j],
+                                                                          n.bmax[0][j], n.bmax[1][j], n.bmax[2][j], r);
+                    if (pass) {
+                        if (held != kQNone) st[kBlock * sp++] = (uint16_t)held;
+                        held = n.e[j];
+                    }
+                }
+                if (held != kQNone) cur = held;
+                else if (sp == sb) done = true;
+                else cur = (int)(int16_t)st[kBlock * --sp];
+            }
+        }
+        // an ended job's hit joins the wave's list
+        const uint64_t fm = __ballot(done && jb.prim >= 0);
+        if (fm != 0) {
+            if (done && jb.prim >= 0) {
+                const int e = ncnt + mbcnt64(fm);
+                qs->res[e] = jb.dist;
+                qs->prim[e] = jb.prim;
+                qs->pair[e] = (uint16_t)owner;
+            }
+            ncnt += __popcll(fm);
+        }
+        if (done) job = false;
+        const uint64_t jm = __ballot(job);
+        if (jm == 0) break;
+        // idle lanes take the bottom entries of lanes with pending entries (k-th idle
+        // lane from the k-th such lane, through a mailbox)
+        const uint64_t vm = __ballot(job && sp > sb);
+        const uint64_t im = __ballot(!job);
+        int m = __popcll(im) < __popcll(vm) ? __popcll(im) : __popcll(vm);
+        if (m > kStealList - jobs) m = kStealList - jobs;
+        if (m > 0) {
+            if (job && sp > sb) {
+                const int rv = mbcnt64(vm);
+                if (rv < m) {
+                    qs->flag[rv] = (uint32_t)st[kBlock * sb] | (uint32_t)owner << 16;
+                    ++sb;
+                }
+            }
+            wave_lds_sync();
+            if (!job) {
+                const int ri = mbcnt64(im);
+                if (ri < m) {
+                    const uint32_t mb = qs->flag[ri];
+                    cur = (int)(int16_t)(mb & 0xffffu);
+                    owner = (int)(mb >> 16);
+                    r = owner_ray(dl, owner, cl);
+                    job = true;
+                    sb = sp = 0;
+                    jb.prim = -1;
+                    jb.dist = 0.0;
+                }
+            }
+            jobs += m;
+            wave_lds_sync();  // the mailbox is reused
+        }
+    }
+    // per ray: the least (distance key, DFS rank) over its list entries
+    wave_lds_sync();
+    Hit out;
+    out.prim = -1;
+    out.dist = 0.0;
+    int orank = 0;
+    for (int e = 0; e < ncnt; ++e) {
+        if (need && (int)qs->pair[e] == lane) {
+            const double d = qs->res[e];
+            const int p = qs->prim[e];
+            const int rk = s.grank[p];
+            const unsigned long long kd = dist_key(d), ko = dist_key(out.dist);
+            if (out.prim < 0 || kd < ko || (kd == ko && rk < orank)) {
+                out.dist = d;
+                out.prim = p;
+                orank = rk;
+            }
+        }
+    }
+    wave_lds_sync();  // QScratch is reused by the next query
+    return out;
+}
+
 #ifndef TPT_GEN_STATS
 #define TPT_GEN_STATS 0
 #endif
@@ -544,7 +684,17 @@ TPT_D int gen_step_t(const DScene& s, const WfState& w, int64_t k, int& phase, B
             atomicAdd(&tpt_walkstat[6], (unsigned long long)wmax);
         }
 #else
-        if (need) group_closest(s, gn, ray, cl, best);
+        if (TPT_WALK_STEAL && gn.b <= -2 && s.ws) {
+            if (need) {  // the owner's ray, for the lanes that take part of its walk
+                dl.at(kGdDx) = ray.d.x; dl.at(kGdDy) = ray.d.y; dl.at(kGdDz) = ray.d.z;
+                dl.at(kGdCl) = __int_as_float(cl);
+                dl.at(kGdOx) = ray.o.x; dl.at(kGdOy) = ray.o.y; dl.at(kGdOz) = ray.o.z;
+            }
+            const Hit wh = walk4_steal(s, -2 - gn.b, need, ray, cl, dl);
+            if (wh.prim >= 0 && (best.prim < 0 || best.dist > wh.dist)) best = wh;
+        } else if (need) {
+            group_closest(s, gn, ray, cl, best);
+        }
 #endif
         pend = 0;
         closest_groups_c(s, gw + 1, s.ngroup, ray, cl, best);  // ... and after it

@@ -2097,6 +2097,8 @@ int tpt_upload_scene(tpt_ctx* c, const tpt_scene_desc* d) {
            o_em = push_array(blob, hs.emitters), o_t = push_array(blob, hs.tnodes),
            o_lf = push_array(blob, hs.leaves), o_gr = push_array(blob, hs.groups), o_ft = push_array(blob, hs.ftris),
            o_q4 = push_array(blob, hs.qnodes);
+    if (hs.grank.size() < hs.tris.size()) hs.grank.resize(hs.tris.size(), 0);
+    const size_t o_rk = push_array(blob, hs.grank);
     if (c->blob) { (void)hipFree(c->blob); c->blob = nullptr; }
     HIP_TRY(c, hipMalloc(&c->blob, blob.size()));
     HIP_TRY(c, hipMemcpy(c->blob, blob.data(), blob.size(), hipMemcpyHostToDevice));
@@ -2119,6 +2121,7 @@ int tpt_upload_scene(tpt_ctx* c, const tpt_scene_desc* d) {
     ds.ngroup = (int)hs.groups.size();
     ds.ftris = lds_full ? ds.tris : (const DTri*)(b + o_ft);
     ds.qnodes = (const QNode4*)(b + o_q4);
+    ds.grank = (const uint16_t*)(b + o_rk);
     ds.lds_full = lds_full;
     ds.nmats = (int)hs.mats.size();
     ds.n_emitters = (int)hs.emitters.size();

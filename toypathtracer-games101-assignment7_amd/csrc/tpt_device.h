@@ -665,6 +665,104 @@ TPT_D Hit traverse_flat_c(const DScene& s, const Ray& r, int cull) {
     closest_groups_c(s, 0, s.ngroup, r, cull, best);
     return best;
 }
+// Connect's shadow walks with work stealing (TPT_CONN_STEAL; see walk4_steal in
+// tpt_bdpt.h for the closest-hit form): lanes of the query whose ray misses the walk
+// group's box, or whose walk has ended, walk subtrees from other lanes' stacks with the
+// owner's ray.  Any hit below the owner's threshold marks the owner shadowed; its other
+// jobs then end.  The answer is the any-hit answer, so the order of the jobs is free.
+#ifndef TPT_CONN_STEAL
+#define TPT_CONN_STEAL 0
+#endif
+TPT_D bool walk4_shadow_steal(const DScene& s, int root, bool need, Ray r, double thr, int cl) {
+    QScratch* qs = wave_qs(s);
+    const int lane = (int)__lane_id();
+    float* rv = reinterpret_cast<float*>(qs->res);  // [slot][lane]: o, d, cull, thr (lo, hi)
+    uint16_t* blocked = qs->pair;
+    uint16_t* st = s.ws + threadIdx.x;
+    wave_lds_sync();
+    if (need) {
+        rv[0 * 64 + lane] = r.o.x; rv[1 * 64 + lane] = r.o.y; rv[2 * 64 + lane] = r.o.z;
+        rv[3 * 64 + lane] = r.d.x; rv[4 * 64 + lane] = r.d.y; rv[5 * 64 + lane] = r.d.z;
+        rv[6 * 64 + lane] = __int_as_float(cl);
+        rv[7 * 64 + lane] = __int_as_float(__double2loint(thr));
+        rv[8 * 64 + lane] = __int_as_float(__double2hiint(thr));
+    }
+    blocked[lane] = 0;
+    wave_lds_sync();
+    int sb = 0, sp = 0, cur = root, owner = lane, jobs = 0;
+    bool job = need;
+    for (;;) {
+        bool done = job && blocked[owner] != 0;
+        if (job && !done) {
+            if (cur < 0) {
+                double dist;
+                if (tri_test(load_gtri(s.gtris + (-1 - cur)), r, cl, dist)) {
+                    const V3 hx = r.o + mul(r.d, (float)dist);
+                    if (dot3(hx - r.o, hx - r.o) < thr) {
+                        blocked[owner] = 1;
+                        done = true;
+                    }
+                }
+                if (!done) {
+                    if (sp == sb) done = true;
+                    else cur = (int)(int16_t)st[kBlock * --sp];
+                }
+            }
+            if (!done && cur >= 0) {
+                const QNode4 n = load_qnode(s.qnodes + cur);
+                int held = kQNone;
+                for (int j = kWalkW - 1; j >= 0; --j) {
+                    const bool pass = n.e[j] != kQNone && slab_hit_finite(n.bmin[0][j], n.bmin[1][j], n.bmin[2][j],
+                                                                          n.bmax[0][j], n.bmax[1][j], n.bmax[2][j], r);
+                    if (pass) {
+                        if (held != kQNone) st[kBlock * sp++] = (uint16_t)held;
+                        held = n.e[j];
+                    }
+                }
+                if (held != kQNone) cur = held;
+                else if (sp == sb) done = true;
+                else cur = (int)(int16_t)st[kBlock * --sp];
+            }
+        }
+        if (done) job = false;
+        if (__ballot(job) == 0) break;
+        const uint64_t vm = __ballot(job && sp > sb);
+        const uint64_t im = __ballot(!job);
+        int m = __popcll(im) < __popcll(vm) ? __popcll(im) : __popcll(vm);
+        if (m > 64 - jobs) m = 64 - jobs;  // a bounded number of steals per query
+        if (m > 0) {
+            if (job && sp > sb) {
+                const int k = mbcnt64(vm);
+                if (k < m) {
+                    qs->flag[k] = (uint32_t)st[kBlock * sb] | (uint32_t)owner << 16;
+                    ++sb;
+                }
+            }
+            wave_lds_sync();
+            if (!job) {
+                const int k = mbcnt64(im);
+                if (k < m) {
+                    const uint32_t mb = qs->flag[k];
+                    cur = (int)(int16_t)(mb & 0xffffu);
+                    owner = (int)(mb >> 16);
+                    r = make_ray(v3(rv[0 * 64 + owner], rv[1 * 64 + owner], rv[2 * 64 + owner]),
+                                 v3(rv[3 * 64 + owner], rv[4 * 64 + owner], rv[5 * 64 + owner]));
+                    cl = __float_as_int(rv[6 * 64 + owner]);
+                    thr = __hiloint2double(__float_as_int(rv[8 * 64 + owner]), __float_as_int(rv[7 * 64 + owner]));
+                    job = true;
+                    sb = sp = 0;
+                }
+            }
+            jobs += m;
+            wave_lds_sync();
+        }
+    }
+    wave_lds_sync();
+    const bool sh = need && blocked[lane] != 0;
+    wave_lds_sync();
+    return sh;
+}
+
 // Shadow query (any hit with |hit - r.o|^2 < thr; r.o is the query's lc, see shadow_ray).
 TPT_D bool shadow_flat_c(const DScene& s, const Ray& r, double thr, int cull) {
     uint64_t mask, any;
@@ -713,7 +811,11 @@ TPT_D bool shadow_flat_c(const DScene& s, const Ray& r, double thr, int cull) {
         if (gn.b >= 0) continue;
         const bool pass =
             !sh && slab_hit_finite(gn.bmin[0], gn.bmin[1], gn.bmin[2], gn.bmax[0], gn.bmax[1], gn.bmax[2], r);
-        if (pass) sh = group_shadow(s, gn, r, r.o, thr, cull);
+        if (TPT_CONN_STEAL && gn.b <= -2 && s.ws) {
+            if (walk4_shadow_steal(s, -2 - gn.b, pass, r, thr, cull)) sh = true;
+        } else if (pass) {
+            sh = group_shadow(s, gn, r, r.o, thr, cull);
+        }
     }
     return sh;
 }

@@ -134,6 +134,7 @@ struct DScene {
     const QNode4* qnodes;     // 4-wide trees of the walk groups
     const DTri* ftris;        // triangle of flat leaf j is ftris[leaves[j].b]
     const DTri* gtris;        // `tris` in HBM, never re-pointed to LDS (the wide walks' global loads)
+    const uint16_t* grank;    // walk-group triangles: rank in the reference's DFS visit order (stealing walks' ties)
     int32_t nleaf;
     int32_t ngroup;
     int32_t flat;             // flat (all-leaves) queries: kFlatShadow | kFlatHit bits, 0 = tree walks

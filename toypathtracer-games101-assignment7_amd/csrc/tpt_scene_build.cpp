@@ -164,6 +164,11 @@ static int build_qtree(HostScene& hs, int p, int& depth) {
         for (int k = 0; k < 3; ++k) { Q.bmin[k][j] = E.bmin[k]; Q.bmax[k][j] = E.bmax[k]; }
         if (E.a < 0) {
             Q.e[j] = E.a;  // -1 - prim
+            // the walk reaches leaves in entry order, subtree by subtree: this is the
+            // reference's DFS rank of the triangle within the group (BVH.cpp:129-132)
+            const size_t prim = (size_t)(-1 - E.a);
+            if (hs.grank.size() < hs.tris.size()) hs.grank.resize(hs.tris.size(), 0);
+            if (prim < hs.grank.size()) hs.grank[prim] = (uint16_t)hs.grank_next++;
         } else {
             int d = 0;
             Q.e[j] = build_qtree(hs, ent[j], d);
@@ -203,6 +208,7 @@ static void split_walk_groups(HostScene& hs, const std::vector<int>& gwalk, cons
             // indices fit the stack's 16-bit entries
             const size_t q0 = hs.qnodes.size();
             int depth = 0;
+            hs.grank_next = 0;
             const int qr = build_qtree(hs, gnode[g], depth);
             const bool fits = (kWalkW - 1) * depth + 1 <= kWalkStack && hs.qnodes.size() <= 32767 &&
                               hs.tris.size() <= 32767;

@@ -15,6 +15,8 @@ struct HostScene {
     std::vector<DNode> groups;  // per object: its box, first leaf (a) and leaf count (b); b < 0: walk group
     std::vector<DTri> ftris;    // flat-only LDS mode: the triangle of each flat leaf, in leaf order
     std::vector<QNode4> qnodes; // 4-wide trees of the walk groups
+    std::vector<uint16_t> grank; // per triangle: rank of its leaf in its walk group's DFS visit order
+    int grank_next = 0;          // (build_qtree's counter, reset per walk group)
     std::vector<float> node_area;
     std::vector<DTri> tris;
     std::vector<DTriX> trix;
