@@ -1506,9 +1506,11 @@ int64_t shard_count(int64_t npix, int64_t begin, int64_t stride) {
 #define TPT_GEN_GRID_Q_WALK 12
 #endif
 #ifndef TPT_GEN_GRID_Q_WALK2
-#define TPT_GEN_GRID_Q_WALK2 10  // ... when two gen kernels run at once (wavefronts of >= 3 iterations: whole
-                                 // frames since round 4).  With the deferred walks, bunny 256 spp, 9 / 10 /
-                                 // 11 / 12 -> 742.0 / 742.1 / 753.9 / 760.4 ms
+#define TPT_GEN_GRID_Q_WALK2 8  // ... when two gen kernels run at once (wavefronts of >= 3 iterations: whole
+                                // frames since round 4).  With the deferred walks, bunny 256 spp, 9 / 10 /
+                                // 11 / 12 -> 742.0 / 742.1 / 753.9 / 760.4 ms; with the stealing walks (round
+                                // 5) 6 / 7 / 8 / 10 -> 659 / 651 / 651 / 684 ms (means of two), configs[4]'s
+                                // 4096-spp frame 7 / 8 / 10 -> 10.39 / 10.38 / 10.93 s
 #endif
 #ifndef TPT_GEN_GRID_Q_WALK_SHARD
 #define TPT_GEN_GRID_Q_WALK_SHARD 11  // ... and for wavefronts of >= 8 iterations (shards of a frame, whose gen
