@@ -1573,8 +1573,10 @@ std::vector<int> wf_schedule(int spp, int nb) {
 #define TPT_CONN_GRID 16384  // connect's grid-stride grid, small flat scenes (Standard BDPT 256 spp: 8192 / 16384 -> 445.4 / 441.2 ms)
 #endif
 #ifndef TPT_CONN_GRID_WALK
-#define TPT_CONN_GRID_WALK 16384  // ... and scenes with walk groups (round 3, bunny BDPT 256 spp: 8192 / 16384 -> 928 / 935 ms;
-                                  // round 5, with the partition: 716.3 / 715.5 ms, its 1/8 shard at 4096 spp 1597 / 1577 ms)
+#define TPT_CONN_GRID_WALK 8192  // ... and scenes with walk groups (round 3, bunny BDPT 256 spp: 8192 / 16384 -> 928 / 935 ms;
+                                 // round 5, with the partition: 716.3 / 715.5 ms, its 1/8 shard at 4096 spp 1597 / 1577 ms;
+                                 // with the stealing gen walks and gen at 8/32: 643 / 655 ms, shard 1351 / 1393 ms,
+                                 // configs[4]'s frame 10.19 / 10.31 s; 8,192 with 8-round partition chunks: 654 ms)
 #endif
 
 // The per-wavefront chain on the connect stream s2: scan, scatter, connect, strategy sums
