@@ -157,9 +157,12 @@ TPT_D V3 path_weight(const DScene& s, const P& paths, int sl, int tl) {
         cst = mul(fl * fc, (float)dabs_(dot3(normal_of(ly.type, ly.N), dir) * dot3(normal_of(cz.type, cz.N), -dir) / (double)d2));
     }
     float wd = 1.0f;
+#ifndef TPT_DIAG_NO_MIS
+#define TPT_DIAG_NO_MIS 0  // diagnostics builds only (timing attribution; wrong images): no MIS chains
+#endif
     // loop A: camera prefix C[0..tl), append L[sl-1], ..., L[0]
     float cur = 1.0f;
-    for (int k = 0; k < sl; ++k) {
+    for (int k = 0; k < (TPT_DIAG_NO_MIS ? 0 : sl); ++k) {
         const int j = sl - 1 - k;
         if (k >= 2) {
             cur *= paths.litq(j, tl + k > 4);
@@ -176,7 +179,7 @@ TPT_D V3 path_weight(const DScene& s, const P& paths, int sl, int tl) {
     }
     // loop B: light prefix L[0..sl), append C[tl-1], ..., C[0]
     cur = 1.0f;
-    for (int k = 0; k < tl; ++k) {
+    for (int k = 0; k < (TPT_DIAG_NO_MIS ? 0 : tl); ++k) {
         const int j = tl - 1 - k;
         const int count = sl + k;
         if (k >= 2) {
