@@ -461,6 +461,15 @@ struct GenDefer {  // [slot][lane] in LDS
 enum { kGdOx = kGdPrim, kGdOy = kGdDlo, kGdOz = kGdDhi };
 constexpr int kStealList = kQC - 64;  // QScratch::res[kStealList, kQC) holds the rays' minima
 TPT_D unsigned long long dist_key(double d) { return (unsigned long long)__double_as_longlong(d) & 0x7fffffffffffffffull; }
+// Does hit a come before hit b in the walk's fold (strict `>` in DFS order): a nearer
+// distance, or the same distance (key: -0.0 ties +0.0) and a lower DFS rank?  The
+// ranks are read only on a tie.
+TPT_D bool hit_before(const DScene& s, const Hit& a, const Hit& b) {
+    if (b.prim < 0) return true;
+    const unsigned long long ka = dist_key(a.dist), kb = dist_key(b.dist);
+    if (ka != kb) return ka < kb;
+    return s.grank[a.prim] < s.grank[b.prim];
+}
 TPT_D Ray owner_ray(const GenDefer& dl, int l, int& cl) {
     const float* b = dl.base + ((int)threadIdx.x & ~63) + l;
     cl = __float_as_int(b[kGdCl * kBlock]);
@@ -480,6 +489,9 @@ TPT_D Hit walk4_steal(const DScene& s, int root, bool need, Ray r, int cl, const
     jb.prim = -1;
     jb.dist = 0.0;
     int ncnt = 0, jobs = __popcll(__ballot(need));
+    Hit own;  // the merged hits of this lane's own ray's jobs that this lane walked
+    own.prim = -1;
+    own.dist = 0.0;
     for (;;) {
         bool done = false;
         if (job) {  // one step of the job's walk (walk4's)
@@ -509,10 +521,12 @@ TPT_D Hit walk4_steal(const DScene& s, int root, bool need, Ray r, int cl, const
                 else cur = (int)(int16_t)st[kBlock * --sp];
             }
         }
-        // an ended job's hit joins the wave's list
-        const uint64_t fm = __ballot(done && jb.prim >= 0);
+        // an ended job's hit: into the lane's own result when the ray is its own, else
+        // onto the wave's list
+        if (done && jb.prim >= 0 && owner == lane && hit_before(s, jb, own)) own = jb;
+        const uint64_t fm = __ballot(done && jb.prim >= 0 && owner != lane);
         if (fm != 0) {
-            if (done && jb.prim >= 0) {
+            if (done && jb.prim >= 0 && owner != lane) {
                 const int e = ncnt + mbcnt64(fm);
                 qs->res[e] = jb.dist;
                 qs->prim[e] = jb.prim;
@@ -555,23 +569,15 @@ TPT_D Hit walk4_steal(const DScene& s, int root, bool need, Ray r, int cl, const
             wave_lds_sync();  // the mailbox is reused
         }
     }
-    // per ray: the least (distance key, DFS rank) over its list entries
+    // per ray: the least (distance key, DFS rank) over its own result and its list entries
     wave_lds_sync();
-    Hit out;
-    out.prim = -1;
-    out.dist = 0.0;
-    int orank = 0;
+    Hit out = own;
     for (int e = 0; e < ncnt; ++e) {
         if (need && (int)qs->pair[e] == lane) {
-            const double d = qs->res[e];
-            const int p = qs->prim[e];
-            const int rk = s.grank[p];
-            const unsigned long long kd = dist_key(d), ko = dist_key(out.dist);
-            if (out.prim < 0 || kd < ko || (kd == ko && rk < orank)) {
-                out.dist = d;
-                out.prim = p;
-                orank = rk;
-            }
+            Hit h;
+            h.dist = qs->res[e];
+            h.prim = qs->prim[e];
+            if (hit_before(s, h, out)) out = h;
         }
     }
     wave_lds_sync();  // QScratch is reused by the next query
