@@ -8,4 +8,4 @@ d=gpurun_out/st1_${tag}_${sc}_${n}
 timeout -k 10 120 rocprofv3 --kernel-trace -d $d -o run --output-format csv -- python scripts/diag/shard_run.py $sc $mo $spp $n 0 2 > $d.log 2>&1 || exit 1
 f=$(find $d -name '*kernel_trace.csv' | head -1)
 echo "== $tag $sc $mo spp $spp N=$n"; grep kernel_ms $d.log
-if grep -q gen_res "$f"; then python scripts/diag/res_timeline.py "$f"; else python scripts/diag/wf_timeline.py "$f" 2; fi
+python scripts/diag/wf_timeline.py "$f" 2

@@ -9,6 +9,9 @@
 #          GRBM_GUI_ACTIVE (the clock the run held)
 #   misc   SALU / LDS / VMEM / SMEM instruction counts and the wait buckets
 #   fetch  FETCH_SIZE ; write  WRITE_SIZE
+#   lane   SQ_THREAD_CYCLES_VALU / SQ_ACTIVE_INST_VALU: VALU lane utilisation (round 6;
+#          counter_defs.yaml's VALUUtilization = THREAD_CYCLES / (64 x ACTIVE_INST_VALU))
+# PASSES="kt lane ..." runs a subset (default: all); NOCOST=1 skips valu_cost.
 # and, once per call, scripts/valu_cost (cycles per wave-instruction of each class).
 # Each step has its own time limit; the script stops at the first failure.
 set -eu
@@ -25,8 +28,15 @@ run() {  # name timeout args...
 }
 P1=SQ_INSTS_VALU,SQ_INSTS_VALU_ADD_F32,SQ_INSTS_VALU_MUL_F32,SQ_INSTS_VALU_FMA_F32,SQ_INSTS_VALU_TRANS_F32,SQ_INSTS_VALU_ADD_F64,SQ_INSTS_VALU_MUL_F64,SQ_INSTS_VALU_FMA_F64
 P2=SQ_INSTS_VALU_TRANS_F64,SQ_INSTS_VALU_INT32,SQ_INSTS_VALU_INT64,SQ_INSTS_VALU_CVT,SQ_ACTIVE_INST_VALU,SQ_WAVE_CYCLES,SQ_BUSY_CYCLES,SQ_WAIT_INST_ANY,GRBM_GUI_ACTIVE,GRBM_COUNT
+P4=SQ_THREAD_CYCLES_VALU,SQ_ACTIVE_INST_VALU,SQ_INSTS_VALU,SQ_INSTS_BRANCH,SQ_WAVE_CYCLES,SQ_WAVES
 P3=SQ_INSTS_SALU,SQ_INSTS_LDS,SQ_INSTS_VMEM_RD,SQ_INSTS_VMEM_WR,SQ_INSTS_SMEM,SQ_WAIT_ANY,SQ_ACTIVE_INST_ANY,SQ_WAVES
-run valu_cost 120 scripts/valu_cost
+passes=${PASSES:-kt valu1 valu2 misc fetch write lane}
+prun() {  # pass workload-name timeout args...: run() when the pass is selected
+  local p=$1; shift
+  case " $passes " in *" $p "*) run "$@" ;; esac
+  return 0
+}
+[ -n "${NOCOST:-}" ] || run valu_cost 120 scripts/valu_cost
 for w in $work; do
   case $w in
     pt)   B="python bench.py --mode pt --steps 1 --warmup 1 --no-cpu" ;;
@@ -37,11 +47,12 @@ for w in $work; do
     c4_smooth) B="python bench.py --mode c4_smooth --steps 1 --warmup 0 --spp 1024 --no-cpu" ;;
     *) echo "unknown workload $w"; exit 2 ;;
   esac
-  run ${w}_kt 240 rocprofv3 --kernel-trace --stats -d "$out/${w}_kt" -o run --output-format csv -- $B
-  run ${w}_valu1 180 rocprofv3 --pmc $P1 --kernel-trace -d "$out/${w}_valu1" -o run --output-format csv -- $B
-  run ${w}_valu2 180 rocprofv3 --pmc $P2 --kernel-trace -d "$out/${w}_valu2" -o run --output-format csv -- $B
-  run ${w}_misc 180 rocprofv3 --pmc $P3 --kernel-trace -d "$out/${w}_misc" -o run --output-format csv -- $B
-  run ${w}_fetch 180 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$out/${w}_fetch" -o run --output-format csv -- $B
-  run ${w}_write 180 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$out/${w}_write" -o run --output-format csv -- $B
+  prun kt ${w}_kt 240 rocprofv3 --kernel-trace --stats -d "$out/${w}_kt" -o run --output-format csv -- $B
+  prun valu1 ${w}_valu1 180 rocprofv3 --pmc $P1 --kernel-trace -d "$out/${w}_valu1" -o run --output-format csv -- $B
+  prun valu2 ${w}_valu2 180 rocprofv3 --pmc $P2 --kernel-trace -d "$out/${w}_valu2" -o run --output-format csv -- $B
+  prun misc ${w}_misc 180 rocprofv3 --pmc $P3 --kernel-trace -d "$out/${w}_misc" -o run --output-format csv -- $B
+  prun fetch ${w}_fetch 180 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$out/${w}_fetch" -o run --output-format csv -- $B
+  prun write ${w}_write 180 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$out/${w}_write" -o run --output-format csv -- $B
+  prun lane ${w}_lane 180 rocprofv3 --pmc $P4 --kernel-trace -d "$out/${w}_lane" -o run --output-format csv -- $B
 done
 echo "=== done $(date +%T)"

@@ -366,40 +366,16 @@ static_assert(kWfChunk * (kMaxLen * (kMaxLen + 1)) < (int64_t(1) << 32), "per-cl
 TPT_D int64_t wf_pixel(const WfState& w, int64_t k) { return w.list ? w.list[k] : w.begin + k * w.stride; }
 TPT_D int tp_pack(int type, int prim) { return (prim + 1) * 4 + type; }
 TPT_D float4* rec_at(float4* rec, int64_t k, int slot) { return rec + ((k * (2 * kMaxLen) + slot) * kRecV); }
-// Stores of the wavefront state.  kWT (the resident gen kernel, whose records are read
-// by kernels that start while it still runs): write-through to memory (agent-scope
-// relaxed atomic stores, `sc1`), so a later `s_waitcnt vmcnt(0)` and a relaxed counter
-// publish them without writing back the whole XCD L2 (MI355X_MICROARCH.md, hand-offs);
-// otherwise plain stores (published by the kernel's end).
-template <bool kWT>
-TPT_D void st2(float* p, float a, float b) {
-    if constexpr (kWT) {
-        const unsigned long long v = (unsigned long long)__float_as_uint(a) | ((unsigned long long)__float_as_uint(b) << 32);
-        __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-        *reinterpret_cast<float2*>(p) = make_float2(a, b);
-    }
-}
-template <bool kWT>
-TPT_D void st4(float4* p, float a, float b, float c, float d) {
-    if constexpr (kWT) {
-        st2<true>(reinterpret_cast<float*>(p), a, b);
-        st2<true>(reinterpret_cast<float*>(p) + 2, c, d);
-    } else {
-        *p = make_float4(a, b, c, d);
-    }
-}
-template <bool kWT = false>
+// Stores of the wavefront state (plain stores, published by the kernel's end).
 TPT_D void rec_store(const WfState& w, int slot, int64_t k, const BVert& v) {
     float4* r = rec_at(w.rec, k, slot);
-    st4<kWT>(r, v.x.x, v.x.y, v.x.z, __builtin_bit_cast(float, tp_pack(v.type, v.prim)));
-    st4<kWT>(r + 1, v.N.x, v.N.y, v.N.z, v.pdf);
-    st4<kWT>(r + 2, v.alpha.x, v.alpha.y, v.alpha.z, __builtin_bit_cast(float, v.mat));
-    st4<kWT>(r + 3, v.q1, v.q8, 0.0f, 0.0f);
+    r[0] = make_float4(v.x.x, v.x.y, v.x.z, __builtin_bit_cast(float, tp_pack(v.type, v.prim)));
+    r[1] = make_float4(v.N.x, v.N.y, v.N.z, v.pdf);
+    r[2] = make_float4(v.alpha.x, v.alpha.y, v.alpha.z, __builtin_bit_cast(float, v.mat));
+    r[3] = make_float4(v.q1, v.q8, 0.0f, 0.0f);
 }
-template <bool kWT = false>
 TPT_D void rec_store_q(const WfState& w, int slot, int64_t k, float q1, float q8) {
-    st2<kWT>(reinterpret_cast<float*>(rec_at(w.rec, k, slot) + 3), q1, q8);
+    *reinterpret_cast<float2*>(rec_at(w.rec, k, slot) + 3) = make_float2(q1, q8);
 }
 
 // One generation step of a lane's sample, for the persistent gen kernel: either
@@ -595,7 +571,7 @@ __device__ unsigned long long tpt_walkstat[8];
 // One generation step (see the comment above gen_step's callers).  Returns 1 when the
 // subpath continues, 0 when it has ended (its vertex count is then i + 1), 2 when the
 // step was deferred (kDefer only; `pend` counts the iterations it has waited).
-template <bool kDefer, bool kWT = false>
+template <bool kDefer>
 TPT_D int gen_step_t(const DScene& s, const WfState& w, int64_t k, int& phase, BVert& prev, BVert& cur, int& i,
                      uint32_t& rs, int& pend, GenDefer dl, int gw) {
     const bool start = phase == 1;
@@ -628,7 +604,7 @@ TPT_D int gen_step_t(const DScene& s, const WfState& w, int64_t k, int& phase, B
         const float ct = (float)dot3(l0.N, wi);
         sr = safe_div(pdf1, ct);
         ray = make_ray(l0.x, wi);
-        rec_store<kWT>(w, kMaxLen, k, l0);
+        rec_store(w, kMaxLen, k, l0);
         cur = l0;
     } else {
         go = !(i >= kMaxLen - 1 || cur.type == T_BG);
@@ -723,7 +699,7 @@ TPT_D int gen_step_t(const DScene& s, const WfState& w, int64_t k, int& phase, B
         nx.pdf = pdf;
         nx.alpha = v3s(0.0f);  // fresh InternalPathVertex (BDPT.hpp:19)
         if (sr != 0.0f) nx.alpha = safe_div(cur.alpha, sr);
-        rec_store<kWT>(w, kMaxLen + 1, k, nx);
+        rec_store(w, kMaxLen + 1, k, nx);
         prev = cur;
         cur = nx;
         i = 1;
@@ -738,10 +714,10 @@ TPT_D int gen_step_t(const DScene& s, const WfState& w, int64_t k, int& phase, B
     nx.pdf = pdf * rr;
     nx.alpha = divs(cur.alpha * safe_div(bsdf, sr), rr);
     const int base = phase == 0 ? 0 : kMaxLen;
-    rec_store<kWT>(w, base + i + 1, k, nx);
+    rec_store(w, base + i + 1, k, nx);
     // path_rev for j = i - 1: Append(P[j]) after last = P[i], Pre = P[i+1]
     const float rev = append_pdf(s, cur.type, cur.mat, cur.x, cur.N, nx.x, prev.type, prev.x, prev.N);
-    rec_store_q<kWT>(w, base + i - 1, k, safe_div(rev * 1.f, prev.pdf), safe_div(rev * .8f, prev.pdf));
+    rec_store_q(w, base + i - 1, k, safe_div(rev * 1.f, prev.pdf), safe_div(rev * .8f, prev.pdf));
     prev = cur;
     cur = nx;
     ++i;

@@ -460,7 +460,7 @@ __global__ __launch_bounds__(kBlock, TPT_PTI_MINWAVES) void tpt_pti_kernel(DScen
 #endif
 #if TPT_GEN_STATS
 constexpr int kGenStatMax = 1 << 16;
-// per wave: kernel (0 queue, 1 resident) | launch ordinal << 8, step iterations, lane-steps, idle
+// per wave: kernel (0: gen) | launch ordinal << 8, step iterations, lane-steps, idle
 // iterations, real-time ticks (100 MHz)
 __device__ unsigned long long tpt_genstats[5 * kGenStatMax];
 __device__ unsigned tpt_genstat_n;
@@ -716,270 +716,6 @@ __global__ __launch_bounds__(kBlock, TPT_GEN_MINWAVES) void tpt_bdpt_gen_kernel(
     gst.end(0, batch);
 #endif
     atomicAdd(w.bounces, nbounce);
-}
-
-// Resident chains (round 5), for shards with no more pixel streams than a share of the
-// chip's resident lanes (1/8 of a 784 x 784 frame: 76,832 streams, 262,144 lanes).  In
-// the queue design above a pixel passes from gen(f) to gen(f + 1) every wavefront, so
-// its chain's current sample sits in one of two half-empty kernels and a SIMD issues
-// about twice the wave-iterations its chains need; at 1/8 of a frame the chains' serial
-// latency (a pixel's spp samples, one after the other: the RNG stream) bounds the shard.
-// Here ONE launch covers every wavefront of the chunk: lane k keeps pixel k and its
-// XorShift32 state for all spp samples and writes sample j into the buffer of its
-// wavefront f (f % kWfBufs), so waves stay dense.  Per lane, inside the loop:
-//   * before its first item of wavefront f >= kWfBufs it waits until fold(f - kWfBufs)
-//     has released that buffer (rfree[f - kWfBufs], set by tpt_bdpt_signal_kernel on
-//     the connect stream; the wait holds this lane only);
-//   * after its last item of wavefront f it counts itself into rdone[f] (an agent-scope
-//     release: its records are written back before the count can be seen), and the
-//     connect stream's tpt_bdpt_wait_kernel holds scan / scatter / connect / fold of
-//     wavefront f until rdone[f] == n.
-// A lane's draws, vertices and stores are the queue kernel's (same gen_step_t, same
-// sample order), so the frame is bit-identical.  No wait can block forever: wavefront
-// f - kWfBufs's items are made by lanes that wait on nothing later than f - kWfBufs, and
-// the connect stream never waits on gen's later wavefronts.  A watchdog (as in the queue
-// kernel) gives up a wait that does not finish, counts the lane into every remaining
-// rdone[] and flags the render.
-#ifndef TPT_GEN_RES_PUB
-// 1: a wave publishes wavefront f once, when its last lane leaves f: one release (XCD L2
-//    write-back) per wave and wavefront, plain stores; 0: every store write-through and
-//    each lane counts itself (measured slower: the write-through acks hold up the loads'
-//    waits)
-#define TPT_GEN_RES_PUB 1
-#endif
-#ifndef TPT_GEN_RES_PRIO
-#define TPT_GEN_RES_PRIO 0
-#endif
-#ifndef TPT_GEN_RES_SLEEP
-#define TPT_GEN_RES_SLEEP 127  // s_sleep units (64 cycles) between a waiting wave's polls
-#endif
-struct ResArgs {
-    const int2* wfi;    // per wavefront: (iterations, leading iterations whose items of its buffer hold the camera vertices)
-    int nf;             // wavefronts
-    int spp;
-    int64_t bstride;    // bytes from one wavefront buffer's arrays to the next one's (a multiple of 2 KB)
-    unsigned* rdone;    // per wavefront: pixel streams done with it
-    int* rfree;         // per wavefront: its buffer has been folded
-    float4* camv;       // per pixel stream: its camera vertex v1 (one record)
-    int lpw;            // pixel streams per wave (lanes lpw..63 of each wave idle)
-};
-template <int kSc>
-__global__ __launch_bounds__(kBlock, TPT_GEN_MINWAVES) void tpt_bdpt_gen_res_kernel(DScene s, WfState w, ResArgs a) {
-    // issue priority over connect's waves on the same SIMD: a chain's samples are serial,
-    // so its latency bounds the shard, and connect's waves fill the issue slots it leaves
-    if (TPT_GEN_RES_PRIO) __builtin_amdgcn_s_setprio(TPT_GEN_RES_PRIO);
-    stage_scene<kSc>(s);
-    __shared__ QScratch qsm[kBlock / 64];
-    s.qs = qsm;
-    s.ws = nullptr;
-    if constexpr (kSc == 2) {
-        __shared__ uint16_t wst[kWalkStack * kBlock];
-        s.ws = wst;
-    }
-    constexpr bool kDef = kSc == 2 && TPT_GEN_DEFER;
-    GenDefer dl{nullptr};
-    int gw = -1;
-    if constexpr (kDef) {
-        __shared__ float gdl[kGenDeferSlots * kBlock];
-        dl.base = gdl;
-        int nw = 0;
-        for (int gi = 0; gi < s.ngroup; ++gi)
-            if (s.groups[gi].b < 0) {
-                gw = gi;
-                ++nw;
-            }
-        if (nw != 1) gw = -1;
-    }
-    const int nn = (int)w.n;
-    // a.lpw streams per wave: sparser waves walk shorter (a wave's iteration lasts as long
-    // as its longest lane's step) and more of them hide each other's latency
-    int k = (int)((blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) * a.lpw + lane_id());
-    if (k >= nn || (int)lane_id() >= a.lpw) k = -1;
-    int f = 0, b = 0, j = 0;  // wavefront, iteration within it, sample
-    // item offset (in records) of wavefront g's buffer from buffer 0 (recomputed where
-    // used: held across the loop it spilled)
-    const int64_t rstride = a.bstride / (int64_t)(2 * kMaxLen * kRecV * sizeof(float4));
-    auto boff_of = [&](int g) { return (int64_t)(g % kWfBufs) * rstride; };
-    int phase = 0, i = 0, cn = 0, pend = 0;
-    uint32_t rs = 0;
-    unsigned long long nbounce = 0;
-    BVert prev, cur;
-    if (k >= 0) {
-        rs = (uint32_t)((int)wf_pixel(w, k) + 1);  // ResetRandom(i + 1), Renderer.cpp:42
-        for (int c = 0; c < 3; ++c) {
-            if (TPT_GEN_RES_PUB) w.acc[3 * k + c] = 0.0f;
-            else __hip_atomic_store(w.acc + 3 * k + c, 0.0f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
-    auto start_sample = [&]() {
-        const int64_t ir = (int64_t)b * nn + k + boff_of(f);
-        BVert c0, c1;
-        const bool cached = b < a.wfi[f].y;
-        if (cached || j > 0) {
-            // v0 is the camera itself (the same for every pixel), v1 the pixel's first hit
-            GlobPaths P;
-            P.rec = cached ? rec_at(w.rec, ir, 0) : a.camv + (int64_t)k * kRecV - kRecV;
-            c0 = camera_v0(s);
-            c1 = P.cam(1);
-        } else {
-            camera_vertices(s, wf_pixel(w, k), c0, c1);
-            float4* cv = a.camv + (int64_t)k * kRecV;
-            cv[0] = make_float4(c1.x.x, c1.x.y, c1.x.z, __builtin_bit_cast(float, tp_pack(c1.type, c1.prim)));
-            cv[1] = make_float4(c1.N.x, c1.N.y, c1.N.z, c1.pdf);
-            cv[2] = make_float4(c1.alpha.x, c1.alpha.y, c1.alpha.z, __builtin_bit_cast(float, c1.mat));
-            cv[3] = make_float4(c1.q1, c1.q8, 0.0f, 0.0f);
-        }
-        if (!cached) {
-            rec_store<!TPT_GEN_RES_PUB>(w, 0, ir, c0);
-            rec_store<!TPT_GEN_RES_PUB>(w, 1, ir, c1);
-        }
-        prev = c0;
-        cur = c1;
-        i = 1;
-        phase = 0;
-    };
-    bool fresh = k >= 0;   // sample j starts at the top of the next step
-    bool bok = true;       // wavefront f's buffer is free (f < kWfBufs: always)
-    uint32_t wait_t0 = 0;  // when this lane started waiting for it (| 1; 0: not yet)
-#if TPT_GEN_STATS
-    GenStat gst;
-    gst.begin();
-#endif
-    constexpr bool kWavePub = TPT_GEN_RES_PUB;
-    const unsigned nl0 = (unsigned)__popcll(__ballot(k >= 0));  // the wave's pixel streams
-    int pub = 0;           // (wave-uniform) the next wavefront this wave publishes
-    bool moved = false;    // this lane left a wavefront since the last publication check
-    // wave publication: every wavefront before the wave's slowest lane's is complete for
-    // the wave's nl0 streams; one release writes their records back, one lane counts them
-    auto publish = [&](int upto) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // keep: the fence's own wait may be dropped
-        if (lane_id() == (unsigned)__builtin_ctzll(__ballot(true)))
-            for (int g = pub; g < upto; ++g) __hip_atomic_fetch_add(a.rdone + g, nl0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        pub = upto;
-    };
-    for (;;) {
-        if (kWavePub && __ballot(moved) != 0) {
-            moved = false;
-            int fm = k >= 0 ? f : a.nf;
-            for (int o = 32; o >= 1; o >>= 1) fm = min(fm, __shfl_xor(fm, o));
-            if (fm > pub) publish(fm);
-        }
-        if (__ballot(k >= 0) == 0) break;
-        if (k >= 0 && !bok) {
-            // relaxed (sc1) poll: gen reads nothing the connect stream wrote, it only must
-            // not overwrite the buffer before connect and fold are done with it
-            bok = __hip_atomic_load(a.rfree + (f - kWfBufs), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
-            if (bok) {
-                wait_t0 = 0;
-            } else if (wait_t0 == 0) {
-                wait_t0 = (uint32_t)__builtin_amdgcn_s_memrealtime() | 1u;
-            } else if (TPT_WATCHDOG && (uint32_t)__builtin_amdgcn_s_memrealtime() - wait_t0 > w.stall_ticks) {
-                atomicOr(w.stall, 1);
-                if (kWavePub) {
-                    f = a.nf;  // the wave counts this stream into every remaining wavefront
-                    moved = true;
-                } else {
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    for (int g = f; g < a.nf; ++g) __hip_atomic_fetch_add(a.rdone + g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                }
-                k = -1;
-            }
-        }
-        const bool run = k >= 0 && bok;
-#if TPT_GEN_STATS
-        gst.step(__ballot(run));
-#endif
-        if (run && fresh) {  // one call site: camera_vertices is inlined once
-            start_sample();
-            fresh = false;
-        }
-        // the whole wave waits for a buffer: back off long (thousands of waves polling a few
-        // flags every 512 cycles took a large share of the memory system)
-        if (__ballot(run) == 0) __builtin_amdgcn_s_sleep(TPT_GEN_RES_SLEEP);
-        if (!run) continue;
-        const int64_t ir = (int64_t)b * nn + k + boff_of(f);
-        int ln = -1;
-#if TPT_GEN_STATS
-        const unsigned long long ts0 = __builtin_amdgcn_s_memrealtime();
-#endif
-        const int gsr = gen_step_t<kDef, !kWavePub>(s, w, ir, phase, prev, cur, i, rs, pend, dl, gw);
-#if TPT_GEN_STATS
-        if (lane_id() == (unsigned)__builtin_ctzll(__ballot(true))) {
-            atomicAdd(&tpt_walkstat[3], __builtin_amdgcn_s_memrealtime() - ts0);
-            atomicAdd(&tpt_walkstat[4], 1ull);
-        }
-#endif
-        if (gsr == 0) {
-            if (phase == 0) {
-                cn = i + 1;
-                phase = 1;
-            } else {
-                ln = i + 1;
-            }
-        }
-        if (ln >= 0) {
-            const int64_t it = (int64_t)b * nn + k, eo = (int64_t)(f % kWfBufs) * a.bstride;
-            int* cnt = reinterpret_cast<int*>(reinterpret_cast<char*>(w.cnt) + eo);
-            unsigned long long* np = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(w.np) + eo);
-            unsigned long long* np2 = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(w.np2) + eo);
-            const int cv = cn | (ln << 16);
-            const unsigned long long v1 = (unsigned long long)(cn - 1) | ((unsigned long long)((cn - 1) * (ln - 1)) << 32),
-                                     v2 = (unsigned long long)(cn - 1) | ((unsigned long long)ln << 32);
-            if (kWavePub) {
-                cnt[it] = cv;
-                np[it] = v1;
-                np2[it] = v2;
-            } else {
-                __hip_atomic_store(cnt + it, cv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(np + it, v1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(np2 + it, v2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-            nbounce += (unsigned long long)(cn + ln);
-            ++j;
-            if (++b == a.wfi[f].x) {  // the lane's last item of wavefront f: hand it to connect
-                if (kWavePub) {
-                    moved = true;
-                } else {
-                    // every store of the hand-off was write-through: drained, they are in
-                    // memory, and a relaxed count publishes them (no L2 write-back)
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    __hip_atomic_fetch_add(a.rdone + f, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                }
-                ++f;
-                b = 0;
-                bok = f < kWfBufs;
-            }
-            if (j >= a.spp) k = -1;
-            else fresh = true;
-        }
-    }
-    if (kWavePub && pub < a.nf) publish(a.nf);
-#if TPT_GEN_STATS
-    gst.end(1, 0);
-#endif
-    atomicAdd(w.bounces, nbounce);
-}
-
-// The connect stream's gate for a resident-chains wavefront: one lane waits until every
-// pixel stream has counted itself into *done (or the watchdog fires: the render is then
-// flagged, and what runs after it reads complete older samples, in bounds).
-__global__ void tpt_bdpt_wait_kernel(const unsigned* done, unsigned n, int* stall, unsigned ticks) {
-    if (threadIdx.x != 0) return;
-    const uint32_t t0 = (uint32_t)__builtin_amdgcn_s_memrealtime();
-    // relaxed poll: the kernels after this one read the wavefront, and each starts with
-    // its own acquire
-    while (__hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < n) {
-        __builtin_amdgcn_s_sleep(32);
-        if (TPT_WATCHDOG && (uint32_t)__builtin_amdgcn_s_memrealtime() - t0 > ticks) {
-            atomicOr(stall, 2);
-            break;
-        }
-    }
-}
-// ... and its release of a folded wavefront's buffer to the resident gen kernel.
-__global__ void tpt_bdpt_signal_kernel(int* flag) {
-    if (threadIdx.x == 0) __hip_atomic_store(flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 
@@ -1315,11 +1051,6 @@ struct tpt_ctx {
     void* wf_mem = nullptr;
     int64_t wf_cap = 0;
     int64_t wf_stride = 0;            // bytes from one wavefront buffer's arrays to the next one's
-    void* res_mem = nullptr;          // resident-chains gen: per-wavefront counters + camera vertices
-    int64_t res_bytes = 0;
-    std::vector<int2> res_wfi;        // host copy of the per-wavefront (iterations, cached) table
-    bool no_resident = false;         // the resident-chains path timed out once on this context: not used again
-    bool resident_used = false;       // the current render used it
     int64_t wf_failed = 0;            // a wavefront allocation of this many items failed (0: none);
                                       // later renders of the same shard size do not retry it
     int64_t wf_failed_count = 0;      // ... for shards of this many pixel streams
@@ -1411,8 +1142,7 @@ int ensure_wf(tpt_ctx* c, int64_t n) {
     auto al = [](int64_t b) { return (b + 255) & ~(int64_t)255; };
     const int64_t b_rec = al(2 * kMaxLen * kRecV * n * 16), b_i = al(n * 4), b_l = al(n * 8),
                   b_own = al(n * maxs * 4), b_res = al(n * maxs * 12), b_acc = al(n * 12);
-    // per buffer: a multiple of one item's records (2 KB), so that buffer b's arrays sit at
-    // the same element offsets from buffer 0's (the resident gen kernel addresses them so)
+    // per buffer: a multiple of one item's records (2 KB)
     const int64_t rec_item = 2 * kMaxLen * kRecV * 16;
     const int64_t per_buf = (b_rec + b_i + 4 * b_l + b_own + b_res + b_acc + rec_item - 1) / rec_item * rec_item;
     const int64_t total = kWfBufs * per_buf + b_l + b_acc;
@@ -1560,15 +1290,6 @@ std::vector<int> wf_schedule(int spp, int nb) {
     return out;
 }
 
-#ifndef TPT_GEN_RES
-#define TPT_GEN_RES 0  // resident-chains gen (tpt_bdpt_gen_res_kernel) for small shards (off: see DESIGN §5.2)
-#endif
-#ifndef TPT_GEN_RES_LPW
-#define TPT_GEN_RES_LPW 32  // ... with this many pixel streams per wave
-#endif
-#ifndef TPT_GEN_RES_Q
-#define TPT_GEN_RES_Q 12  // ... for shards whose waves take at most this many 32nds of the chip's resident ones
-#endif
 #ifndef TPT_CONN_GRID
 #define TPT_CONN_GRID 16384  // connect's grid-stride grid, small flat scenes (Standard BDPT 256 spp: 8192 / 16384 -> 445.4 / 441.2 ms)
 #endif
@@ -1578,112 +1299,6 @@ std::vector<int> wf_schedule(int spp, int nb) {
                                  // with the stealing gen walks and gen at 8/32: 643 / 655 ms, shard 1351 / 1393 ms,
                                  // configs[4]'s frame 10.19 / 10.31 s; 8,192 with 8-round partition chunks: 654 ms)
 #endif
-
-// The per-wavefront chain on the connect stream s2: scan, scatter, connect, strategy sums
-// and fold, the periodic splat fold; `it0` is the wavefront's first sample iteration.
-int launch_wavefront_tail(tpt_ctx* c, hipStream_t s2, const WfState& w, void* scan_tmp, int it0, int spp, float inv,
-                          float* dsplat) {
-    const size_t shmem = (size_t)c->ds.lds_bytes;
-    const unsigned iblocks = (unsigned)((w.ni + kBlock - 1) / kBlock), pblocks = (unsigned)((w.n + kBlock - 1) / kBlock);
-    const unsigned cblocks = (unsigned)std::min<int64_t>(c->sc == 2 ? TPT_CONN_GRID_WALK : TPT_CONN_GRID,
-                                                         (w.ni * 24 + kBlock - 1) / kBlock + 1);
-    const auto conn_k = c->sc == 2 ? tpt_bdpt_conn_kernel<2> : c->sc == 1 ? tpt_bdpt_conn_kernel<1> : tpt_bdpt_conn_kernel<0>;
-    size_t bytes = c->scan_bytes;
-    HIP_TRY(c, rocprim::inclusive_scan(scan_tmp, bytes, w.np, w.incl, (size_t)w.ni, rocprim::plus<unsigned long long>(), s2));
-    bytes = c->scan_bytes;
-    HIP_TRY(c, rocprim::inclusive_scan(scan_tmp, bytes, w.np2, w.incl2, (size_t)w.ni, rocprim::plus<unsigned long long>(), s2));
-    hipLaunchKernelGGL(tpt_bdpt_scatter_kernel, dim3(iblocks), dim3(kBlock), 0, s2, w, c->queue);
-    hipLaunchKernelGGL(conn_k, dim3(cblocks), dim3(kBlock), shmem, s2, c->ds, w, dsplat ? c->splat_part : nullptr);
-    if (w.nb == 1) {
-        hipLaunchKernelGGL(tpt_bdpt_fold_kernel, dim3(pblocks), dim3(kBlock), 0, s2, w, inv);
-    } else {
-        hipLaunchKernelGGL(tpt_bdpt_isum_kernel, dim3(iblocks), dim3(kBlock), 0, s2, w);
-        hipLaunchKernelGGL(tpt_bdpt_fold_items_kernel, dim3(pblocks), dim3(kBlock), 0, s2, w, inv);
-    }
-    if (dsplat && ((it0 + w.nb) / TPT_SPLAT_FOLD_SPP > it0 / TPT_SPLAT_FOLD_SPP || it0 + w.nb >= spp)) {
-        const int64_t nf = (int64_t)c->hs.width * c->hs.height * 3;
-        hipLaunchKernelGGL(tpt_splat_fold_kernel, dim3((unsigned)std::min<int64_t>(4096, (nf + 255) / 256)), dim3(256), 0,
-                           s2, dsplat, c->splat_part, nf);
-    }
-    return TPT_OK;
-}
-
-// Resident chains (tpt_bdpt_gen_res_kernel): one gen launch for the whole chunk on
-// c->stream, one lane per pixel stream; per wavefront f on the connect stream: wait for
-// rdone[f] == count, the wavefront's tail, then release its buffer (rfree[f]).  Needs the
-// two streams to run concurrently (distinct hardware queues, as a context's streams are
-// when it is created with fewer than GPU_MAX_HW_QUEUES - 2 other streams in the process);
-// otherwise gen's first buffer wait times out (watchdog), the render fails with
-// TPT_E_DEVICE and the context stops using this path.
-int launch_bdpt_resident(tpt_ctx* c, int spp, int64_t begin, int64_t stride, int64_t count, const int64_t* dlist,
-                         float* drows, float* dsplat, int nb) {
-    const size_t shmem = (size_t)c->ds.lds_bytes;
-    hipStream_t s2 = c->stream2;
-    const std::vector<int> sched = wf_schedule(spp, nb);
-    const int nf = (int)sched.size();
-    c->res_wfi.assign(nf, int2{0, 0});
-    int cam_nb[kWfBufs] = {};
-    for (int f = 0; f < nf; ++f) {
-        const int b = f % kWfBufs;
-        c->res_wfi[f] = int2{sched[f], cam_nb[b]};
-        cam_nb[b] = std::max(cam_nb[b], sched[f]);
-    }
-    auto al = [](int64_t x) { return (x + 255) & ~(int64_t)255; };
-    const int64_t need = al((int64_t)nf * 8) + 2 * al((int64_t)nf * 4) + count * kRecV * 16;
-    if (c->res_bytes < need) {
-        if (c->res_mem) (void)hipFree(c->res_mem);
-        c->res_mem = nullptr;
-        c->res_bytes = 0;
-        HIP_TRY(c, hipMalloc(&c->res_mem, need));
-        c->res_bytes = need;
-    }
-    char* p = (char*)c->res_mem;
-    int2* wfi = (int2*)p;
-    p += al((int64_t)nf * 8);
-    unsigned* rdone = (unsigned*)p;
-    int* rfree = (int*)(p + al((int64_t)nf * 4));
-    float4* camv = (float4*)(p + 2 * al((int64_t)nf * 4));
-    HIP_TRY(c, hipMemcpyAsync(wfi, c->res_wfi.data(), (size_t)nf * sizeof(int2), hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(c, hipMemsetAsync(rdone, 0, (size_t)(2 * al((int64_t)nf * 4)), c->stream));
-    HIP_TRY(c, hipEventRecord(c->ev_start, c->stream));
-    HIP_TRY(c, hipStreamWaitEvent(s2, c->ev_start, 0));
-    auto prep = [&](WfState w, int nbf) {
-        w.list = dlist;
-        w.begin = begin;
-        w.stride = stride;
-        w.n = count;
-        w.nb = nbf;
-        w.ni = (int64_t)nbf * count;
-        w.bounces = c->counters;
-        w.stall = reinterpret_cast<int*>(c->counters + 4);
-        w.stall_ticks = c->stall_ticks;
-        w.drop_k = c->drop_k;
-        w.conc = 0;
-        w.cam_nb = 0;
-        return w;
-    };
-    const unsigned pblocks = (unsigned)((count + kBlock - 1) / kBlock);
-    const int lpw = TPT_GEN_RES_LPW;
-    const int64_t per_block = (int64_t)(kBlock / 64) * lpw;
-    const unsigned gblocks = (unsigned)((count + per_block - 1) / per_block);
-    const auto gen_k = c->sc == 2 ? tpt_bdpt_gen_res_kernel<2> : c->sc == 1 ? tpt_bdpt_gen_res_kernel<1> : tpt_bdpt_gen_res_kernel<0>;
-    const WfState w0 = prep(c->wf[0], nb);
-    hipLaunchKernelGGL(gen_k, dim3(gblocks), dim3(kBlock), shmem, c->stream, c->ds, w0,
-                       ResArgs{wfi, nf, spp, c->wf_stride, rdone, rfree, camv, lpw});
-    const float inv = 1.0f / spp;
-    for (int f = 0, it0 = 0; f < nf; it0 += sched[f], ++f) {
-        const WfState w = prep(c->wf[f % kWfBufs], sched[f]);
-        hipLaunchKernelGGL(tpt_bdpt_wait_kernel, dim3(1), dim3(64), 0, s2, rdone + f, (unsigned)count, w.stall,
-                           c->stall_ticks);
-        const int rc = launch_wavefront_tail(c, s2, w, c->scan_tmp_g[0], it0, spp, inv, dsplat);
-        if (rc) return rc;
-        hipLaunchKernelGGL(tpt_bdpt_signal_kernel, dim3(1), dim3(64), 0, s2, rfree + f);
-    }
-    HIP_TRY(c, hipEventRecord(c->ev_fold[0], s2));
-    HIP_TRY(c, hipStreamWaitEvent(c->stream, c->ev_fold[0], 0));
-    hipLaunchKernelGGL(tpt_bdpt_out_kernel, dim3(pblocks), dim3(kBlock), 0, c->stream, w0, drows, dlist ? 1 : 0);
-    return TPT_OK;
-}
 
 // The BDPT sample loop over `count` (<= kWfChunk) pixel streams, as wavefronts of
 // nb = wf_iters(count, spp) sample iterations each.
@@ -1702,16 +1317,6 @@ int launch_bdpt_chunk(tpt_ctx* c, int spp, int64_t begin, int64_t stride, int64_
     // gen(f + 2) only after fold(f).  Per pixel the order is kept: gen(f) samples after
     // gen(f - 1) (rngseq), fold is sequential on s2 (acc, splat).
     const int nb = (int)std::min<int64_t>(wf_iters(count, spp), std::max<int64_t>(1, c->wf_cap / count));
-    if (TPT_GEN_RES && !TPT_BDPT_SERIAL && !c->no_resident) {
-        int per_cu = 0;
-        const auto gk = c->sc == 2 ? tpt_bdpt_gen_res_kernel<2> : c->sc == 1 ? tpt_bdpt_gen_res_kernel<1> : tpt_bdpt_gen_res_kernel<0>;
-        HIP_TRY(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)gk, kBlock, shmem));
-        const int64_t lanes = (int64_t)std::max(per_cu, 1) * std::max(c->num_cu, 1) * kBlock * TPT_GEN_RES_LPW / 64;
-        if (count * 32 <= lanes * TPT_GEN_RES_Q) {
-            c->resident_used = true;
-            return launch_bdpt_resident(c, spp, begin, stride, count, dlist, drows, dsplat, nb);
-        }
-    }
     hipStream_t s2 = TPT_BDPT_SERIAL ? c->stream : c->stream2;
     // The second gen stream only where wavefronts hold several iterations (small
     // shards: a lane runs nb samples of one pixel, so gen's tail is long).  For a
@@ -1860,7 +1465,6 @@ int launch(tpt_ctx* c, int mode, int flags, int spp, int64_t begin, int64_t stri
         c->drop_k = dk && *dk ? std::atoi(dk) : -1;
         c->stall_ticks = dt && *dt ? (unsigned)std::strtoul(dt, nullptr, 10) : kStallTicks;
 #endif
-        c->resident_used = false;
         // Shards larger than kWfChunk pixel streams run as consecutive chunks.
         const int64_t chunk = std::min(count, kWfChunk), last = count - (count - 1) / kWfChunk * kWfChunk;
         if (dsplat) {
@@ -1913,11 +1517,6 @@ int launch(tpt_ctx* c, int mode, int flags, int spp, int64_t begin, int64_t stri
     if (mode == TPT_MODE_BDPT) {
         int stall = 0;
         HIP_TRY(c, hipMemcpy(&stall, c->counters + 4, sizeof(stall), hipMemcpyDeviceToHost));
-        if (stall && c->resident_used) {
-            c->no_resident = true;  // the streams did not run concurrently: use the queue design from now on
-            return fail(c, TPT_E_DEVICE, "BDPT: a resident gen lane or the connect stream timed out waiting for the "
-                                         "other (are the context's streams on distinct hardware queues?)");
-        }
         if (stall) return fail(c, TPT_E_DEVICE, "BDPT: a gen lane timed out waiting for the previous wavefront");
     }
     if (st) {
@@ -2037,8 +1636,7 @@ void tpt_destroy(tpt_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (void* p : {(void*)c->blob, (void*)c->rgb, (void*)c->splat, (void*)c->splat_part, (void*)c->list, (void*)c->rows, (void*)c->counters,
-                    (void*)c->queue, c->res_mem,
-                    c->wf_mem, c->scan_tmp})
+                    (void*)c->queue, c->wf_mem, c->scan_tmp})
         if (p) (void)hipFree(p);
     if (c->stream2) (void)hipStreamSynchronize(c->stream2);
     if (c->stream3) (void)hipStreamSynchronize(c->stream3);
