@@ -94,6 +94,7 @@ def parse():
     ap.add_argument("--no-c5", action="store_true", help="default line without the c5 sub-object")
     ap.add_argument("--no-shard-model", action="store_true", help="default line without the shard_model sub-object")
     ap.add_argument("--shard-only", action="store_true", help="print the shard_model object alone (A/B runs)")
+    ap.add_argument("--shard-keys", default=None, help="--shard-only: comma list of the shard-model legs (pt,bdpt,c5)")
     ap.add_argument("--sample-seed", action="store_true",
                     help="--mode pt|pti only: per-sample seeding (TPT_FLAG_SAMPLE_SEED), a non-replay throughput mode")
     ap.add_argument("--cpu-threads", type=int, default=None)
@@ -551,7 +552,10 @@ class Runner:
                        "(pixels i = r mod N, Renderer.cpp:38) rendered alone on this GPU; eff = T_full / "
                        "(N x slowest shard), kernel time (HIP events); the reduce (one 7.4 / 14.7 MB RCCL "
                        "reduce) is not modelled", "ns": list(SHARD_NS)}
+        keys = self.args.shard_keys.split(",") if getattr(self.args, "shard_keys", None) else None
         for key, spp in SHARD_MODEL:
+            if keys is not None and key not in keys:
+                continue
             scene, mode, _ = WORKLOADS[key]
             if self.scene != scene:
                 self.ctx.upload(pytpt.Preset(scene))

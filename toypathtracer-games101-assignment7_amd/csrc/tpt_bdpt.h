@@ -125,8 +125,15 @@ TPT_D bool shadow_v(const DScene& s, const BVert& v1, const BVert& v2) {
 // BDPTPath::PathWeight (BDPT.cpp:173-259) for light sub-length sl, camera sub-length tl.
 // Paths are read through an accessor P: P::cam(j), P::lit(j) return vertex records,
 // P::camq / P::litq the cached MIS factors (rr .8 when `r8`).
-template <class P>
+// kCls >= 0: the caller's strategies are all of one task class (tpt_bdpt_scatter_kernel's
+// runs: 0 s = 0, 1 t > 1 and s > 1, 2 t > 1 and s = 1, 3 t = 1), so the branches of the
+// other classes fold away (the same float ops in the same order for the strategies run).
+template <int kCls = -1, class P>
 TPT_D V3 path_weight(const DScene& s, const P& paths, int sl, int tl) {
+    if constexpr (kCls == 0) __builtin_assume(sl == 0 && tl >= 2);
+    if constexpr (kCls == 1) __builtin_assume(sl >= 2 && tl >= 2);
+    if constexpr (kCls == 2) __builtin_assume(sl == 1 && tl >= 2);
+    if constexpr (kCls == 3) __builtin_assume(tl == 1 && sl >= 1);
     const int z = tl - 1;
     const BVert cz = paths.cam(z);
     if (cz.type == T_BG) return sl == 0 ? cz.alpha * v3(s.bg[0], s.bg[1], s.bg[2]) : v3s(0.0f);
@@ -425,7 +432,8 @@ struct GenDefer {  // [slot][lane] in LDS
 // of smallest DFS rank; the jobs' hits are then merged per ray by (distance, DFS rank)
 // (HostScene::grank), which is exactly the sequential fold's answer: its first
 // minimum.  (The merge is a wave-uniform scan of the list by each owner; a version
-// with LDS atomic minima lost hits and was not kept.)  The walk group's leaves all follow the flat groups before it in the DFS
+// with LDS atomic minima lost hits -- why: DESIGN.md §5.2 -- and was not kept;
+// tests/test_steal_walk.py runs this function on an emulated wave.)  The walk group's leaves all follow the flat groups before it in the DFS
 // order and precede the ones after, so the caller folds the merged hit into `best`
 // with the same strict `>`.  Distances are finite (finite rays, |det| >= 1e-4), and
 // -0.0 ties +0.0 as in the reference (the key clears the sign; the winner's own bits
@@ -435,7 +443,7 @@ struct GenDefer {  // [slot][lane] in LDS
 #endif
 // the origin's slots while a walk runs (their parked values are in registers by then)
 enum { kGdOx = kGdPrim, kGdOy = kGdDlo, kGdOz = kGdDhi };
-constexpr int kStealList = kQC - 64;  // QScratch::res[kStealList, kQC) holds the rays' minima
+constexpr int kStealList = kQC - 64;  // jobs per walk at most, so the stolen jobs' hit list fits QScratch::res
 TPT_D unsigned long long dist_key(double d) { return (unsigned long long)__double_as_longlong(d) & 0x7fffffffffffffffull; }
 // Does hit a come before hit b in the walk's fold (strict `>` in DFS order): a nearer
 // distance, or the same distance (key: -0.0 ties +0.0) and a lower DFS rank?  The

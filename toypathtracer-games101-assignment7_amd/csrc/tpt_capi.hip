@@ -771,6 +771,7 @@ __global__ __launch_bounds__(kBlock) void tpt_bdpt_scatter_kernel(WfState w, uns
 
 // One strategy (task g) of connect: PathWeight, the result at its task index (t > 1)
 // or the splat of the wave (t = 1; call with every lane of the wave).
+template <int kCls = -1>
 TPT_D void conn_task(const DScene& s, const WfState& w, float* __restrict__ splat, int64_t g, bool on, V3 eye) {
     V3 v = v3s(0.0f), lx = eye;
     bool sp = false;
@@ -780,7 +781,7 @@ TPT_D void conn_task(const DScene& s, const WfState& w, float* __restrict__ spla
         const int t = (int)((tk >> 22) & 31), sl = (int)(tk >> 27);
         GlobPaths P;
         P.rec = rec_at(w.rec, k, 0);
-        v = vmax0(path_weight(s, P, sl, t));
+        v = vmax0(path_weight<kCls>(s, P, sl, t));
         if (t > 1) {  // the result stays in task order; fold finds it from (t, s)
             w.res[3 * g] = v.x;
             w.res[3 * g + 1] = v.y;
@@ -791,7 +792,8 @@ TPT_D void conn_task(const DScene& s, const WfState& w, float* __restrict__ spla
         }
     }
     // t = 1: DrawToImage of the light vertex (BDPT.cpp:303-305), whole wave
-    if (splat) splat_wave(s, sp, lx, eye, v, splat);
+    if (kCls < 0 || kCls == 3)
+        if (splat) splat_wave(s, sp, lx, eye, v, splat);
 }
 
 // Walker partition (round 4).  For a scene with walk groups the shadow query of a
@@ -889,6 +891,48 @@ __global__ __launch_bounds__(kBlock, TPT_CONN_MINWAVES) void tpt_bdpt_conn_kerne
             }
             wave_lds_sync();  // the next chunk reuses srt
         }
+    }
+}
+
+// Class kernels (round 6, TPT_CONN_CLASS, small flat scenes; OFF: measured slower).  The
+// emission-only run (s = 0: no connection, no shadow query, one MIS chain) needs 58
+// VGPRs where the other classes need 128 (PathWeight compiled per class,
+// path_weight<kCls>: the s = 1 and t = 1 forms even spill 32 / 92 B/lane at 128), so it
+// can run in a launch of its own at TPT_CONN_W0 waves per SIMD beside the generic kernel
+// for the other three runs.  Same tasks, same results at the same task indices, same
+// splats (the c3 pins passed on the GPU), but Standard BDPT 256 spp went 429.6-430.9 ->
+// 435.1-436.5 ms (8 waves; 6 waves 436.3-437.1 ms): the second launch's drain per
+// wavefront costs more than the emission strategies' occupancy gains.
+#ifndef TPT_CONN_CLASS
+#define TPT_CONN_CLASS 0
+#endif
+#ifndef TPT_CONN_W0
+#define TPT_CONN_W0 8  // waves per SIMD of the s = 0 launch
+#endif
+// [begin, end) of task run c (0 .. 3) of the wavefront's task list; c = -2: runs 1 .. 3
+TPT_D void class_range(const WfState& w, int c, int64_t& b, int64_t& e) {
+    const unsigned long long t1 = w.incl[w.ni - 1], t2 = w.incl2[w.ni - 1];
+    const int64_t n[4] = {(int64_t)(t1 & 0xffffffffull), (int64_t)(t1 >> 32), (int64_t)(t2 & 0xffffffffull),
+                          (int64_t)(t2 >> 32)};
+    const int c0 = c < 0 ? 1 : c, c1 = c < 0 ? 3 : c;
+    b = 0;
+    for (int i = 0; i < c0; ++i) b += n[i];
+    e = b;
+    for (int i = c0; i <= c1; ++i) e += n[i];
+}
+template <int kSc, int kCls>
+__global__ __launch_bounds__(kBlock, kCls == 0 ? TPT_CONN_W0 : TPT_CONN_MINWAVES) void tpt_bdpt_conn_cls_kernel(
+        DScene s, WfState w, float* __restrict__ splat) {
+    stage_scene<kSc>(s);
+    __shared__ QScratch qsm[kBlock / 64];
+    s.qs = qsm;
+    s.ws = nullptr;
+    int64_t b, e;
+    class_range(w, kCls, b, e);
+    const V3 eye = v3(s.eye[0], s.eye[1], s.eye[2]);
+    for (int64_t g0 = b + (int64_t)blockIdx.x * kBlock + (threadIdx.x & ~63); g0 < e; g0 += (int64_t)gridDim.x * kBlock) {
+        const int64_t g = g0 + lane_id();
+        conn_task<kCls < 0 ? -1 : kCls>(s, w, splat, g, g < e, eye);
     }
 }
 
@@ -1390,7 +1434,22 @@ int launch_bdpt_chunk(tpt_ctx* c, int spp, int64_t begin, int64_t stride, int64_
         hipLaunchKernelGGL(tpt_bdpt_scatter_kernel, dim3(iblocks), dim3(kBlock), 0, gs[gsi], w, queue);
         HIP_TRY(c, hipEventRecord(c->ev_gen[b], gs[gsi]));
         HIP_TRY(c, hipStreamWaitEvent(s2, c->ev_gen[b], 0));
-        hipLaunchKernelGGL(conn_k, dim3(cblocks), dim3(kBlock), shmem, s2, c->ds, w, dsplat ? c->splat_part : nullptr);
+#if TPT_CONN_CLASS
+        if (c->sc != 2) {  // s = 0 in its own launch (tpt_bdpt_conn_cls_kernel)
+            float* sp = dsplat ? c->splat_part : nullptr;
+            const dim3 g0((unsigned)std::min<int64_t>(TPT_CONN_GRID, (w.ni * 6 + kBlock - 1) / kBlock + 1));
+            if (c->sc == 1) {
+                hipLaunchKernelGGL((tpt_bdpt_conn_cls_kernel<1, -2>), dim3(cblocks), dim3(kBlock), shmem, s2, c->ds, w, sp);
+                hipLaunchKernelGGL((tpt_bdpt_conn_cls_kernel<1, 0>), g0, dim3(kBlock), shmem, s2, c->ds, w, sp);
+            } else {
+                hipLaunchKernelGGL((tpt_bdpt_conn_cls_kernel<0, -2>), dim3(cblocks), dim3(kBlock), shmem, s2, c->ds, w, sp);
+                hipLaunchKernelGGL((tpt_bdpt_conn_cls_kernel<0, 0>), g0, dim3(kBlock), shmem, s2, c->ds, w, sp);
+            }
+        } else
+#endif
+        {
+            hipLaunchKernelGGL(conn_k, dim3(cblocks), dim3(kBlock), shmem, s2, c->ds, w, dsplat ? c->splat_part : nullptr);
+        }
         if (w.nb == 1) {
             hipLaunchKernelGGL(tpt_bdpt_fold_kernel, dim3(pblocks), dim3(kBlock), 0, s2, w, inv);
         } else {

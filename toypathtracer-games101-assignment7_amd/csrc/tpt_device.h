@@ -35,9 +35,11 @@ TPT_D Ray make_ray(V3 o, V3 d) {
     Ray r;
     r.o = o;
     r.d = d;
-#if TPT_FAST_RCP
+#if TPT_FAST_RCP && !defined(TPT_HOST_EMU)
     // rcp_fast_f32 equals the IEEE quotient on its range (tpt_devmath.h); a wave with a
-    // component outside it (0, denormal, huge: rare) divides.
+    // component outside it (0, denormal, huge: rare) divides.  (The host emulation of
+    // tests/native/wave_emu.h divides: both forms give the same bits, and its waves do not
+    // model a ballot reached by only some lanes, as owner_ray's call in walk4_steal is.)
     if (__ballot(!(rcp_fast_ok(d.x) & rcp_fast_ok(d.y) & rcp_fast_ok(d.z))) == 0) {
         r.inv = v3(rcp_fast_f32(d.x), rcp_fast_f32(d.y), rcp_fast_f32(d.z));
         return r;
