@@ -30,10 +30,11 @@ rocprofv3 SQ_INSTS_VALU_* counts x the cycles per wave-instruction measured on
 MI355X by scripts/valu_cost.hip; `achieved` divides that by the kernel's average
 duration measured live here (HIP events inside libtpt on the stream the kernel runs
 on); `peak` = 1,024 SIMDs x the clock the profiled run held (GRBM_GUI_ACTIVE).
-roofline_hbm_model: SURVEY §8(d)'s modelled HBM yardstick (algorithmic scene-fetch
-bytes / kernel time / 8 TB/s); `traffic` is the measured memory-side bytes per launch
-(profiles/traffic.json).  roofline_hbm_measured: those measured bytes (rocprofv3
-FETCH_SIZE / WRITE_SIZE of the profiled build) / the live kernel time / 8 TB/s.  An N-rank
+scene_fetch_model (was roofline_hbm_model until round 5): SURVEY §8(d)'s algorithmic
+scene-fetch bytes / kernel time, with reuse_factor = that rate / 8 TB/s -- the reads are
+served from LDS / L2, so it is no roofline (a "frac" above 1 read as a violated bound).
+roofline_hbm_measured: the measured memory-side bytes (rocprofv3 FETCH_SIZE /
+WRITE_SIZE of the profiled build) / the live kernel time / 8 TB/s.  An N-rank
 line adds `ranks` (device PCI ids, kernel and reduce ms per rank); every line ends with a
 compact per-config `summary`.
 
@@ -228,22 +229,37 @@ def valu_roofline(key, kernel_ms, samples):
         isa = sum(n * ISA_CYCLES.get(c, 2.0) for c, n in cls.items()) + 2.0 * model.get("other_insts_per_launch", 0)
         out["issue_cycles_per_launch_isa"] = round(isa * shard_frac)
         out["frac_at_isa_rate"] = round(isa * shard_frac / (ms / 1e3) / 1e9 / peak, 4)
+    # lane utilisation (round 6): the share of a VALU wave-instruction's 64 lanes that
+    # work (SQ_THREAD_CYCLES_VALU / (64 x SQ_ACTIVE_INST_VALU)); the issue fraction
+    # counts wave-instructions whatever their lanes, so frac x lane_util is the fraction
+    # of the SIMDs' lane-cycles spent on useful lanes (issue-cycle weighted over BDPT's
+    # kernels)
+    lu = model.get("lane_util")
+    if lu:
+        out["lane_util"] = lu
+        out["frac_lane_weighted"] = round(achieved / peak * lu, 4)
+        out["lane_source"] = model.get("lane_source")
     if len(model.get("per_kernel", {})) > 1:  # BDPT: a sequence of kernels on two streams
         out["per_kernel_profiled"] = model["per_kernel"]
     return out
 
 
-def hbm_model(scene, mode, kernel_ms, samples, traffic_key):
+def scene_fetch_model(scene, mode, kernel_ms, samples, traffic_key):
+    """SURVEY §8(d)'s algorithmic scene-fetch bytes (B_ALG) over the kernel time: a MODEL
+    of the reference traversal's reads, not a bound.  The scene is LDS/L2-resident, so the
+    rate exceeds the HBM peak; reuse_factor = rate / 8 TB/s says by how much the on-chip
+    memories multiply HBM here.  The HBM roofline is roofline_hbm_measured."""
     b_alg = B_ALG.get((scene, "pt" if mode == "pti" else mode))
     if not b_alg:
         return None
     achieved = samples * b_alg / (kernel_ms / 1e3) / 1e9
     t = _load_json("traffic.json").get(traffic_key)
-    return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": float(t["bytes_per_launch"]) if t else None,
+    return {"achieved": round(achieved, 1), "unit": "GB/s", "reuse_factor": round(achieved / HBM_PEAK_GBS, 4),
+            "hbm_peak": HBM_PEAK_GBS, "measured_traffic": float(t["bytes_per_launch"]) if t else None,
             "bytes_per_sample_alg": b_alg, "samples_per_launch": samples,
-            "note": "MODEL (SURVEY 8d): algorithmic scene-fetch bytes / kernel time; the scene is LDS/L2-resident, "
-                    "so frac > 1 is cache reuse, not a violated bound; traffic = measured memory-side bytes per launch"}
+            "note": "MODEL (SURVEY 8d): algorithmic scene-fetch bytes / kernel time, served from LDS / L2; "
+                    "reuse_factor = that rate / the HBM peak (not a roofline fraction); measured_traffic = "
+                    "memory-side bytes per launch (roofline_hbm_measured prices them)"}
 
 
 def _free_port():
@@ -253,23 +269,52 @@ def _free_port():
         return so.getsockname()[1]
 
 
+def _apply_visible(devs, spec):
+    """The devices a *_VISIBLE_DEVICES value selects from `devs` (a list of (ordinal-free)
+    device records with a "uuid"): comma-separated ordinals into `devs` or GPU-<uuid>
+    tokens; duplicates count once, and -- as the HIP/ROCr parsers do -- the list ends at
+    the first token that names no device (out of range, unknown uuid, garbage)."""
+    out = []
+    for tok in spec.split(","):
+        tok = tok.strip()
+        if not tok:
+            break
+        d = None
+        if tok.isdigit():
+            i = int(tok)
+            d = devs[i] if i < len(devs) else None
+        elif tok.upper().startswith("GPU-"):
+            d = next((x for x in devs if x.get("uuid") and x["uuid"].lower() == tok[4:].lower()), None)
+        if d is None:
+            break
+        if d not in out:
+            out.append(d)
+    return out
+
+
 def visible_gpus(root=None):
     """GPUs this process may open, counted WITHOUT the HIP runtime (the launcher must
     not initialise the GPU before it starts the ranks): the kfd topology nodes that
     have SIMDs and a DRM render node this user can open (/dev/dri/renderD<minor>, what
-    ROCr opens), capped by ROCR_/HIP_/CUDA_VISIBLE_DEVICES.  Returns (count, source),
-    or (None, reason) when there is no such view; then amdsmi is tried, and nothing
-    else: torch.cuda.device_count() may fall back to hipGetDeviceCount.
-    `root` (tests: TPT_BENCH_SYSFS_ROOT) prefixes /sys and /dev."""
+    ROCr opens), then narrowed by ROCR_VISIBLE_DEVICES and HIP_VISIBLE_DEVICES (or
+    CUDA_VISIBLE_DEVICES when HIP's is unset), each an ordered list of ordinals into the
+    devices left by the previous level or GPU-<uuid> tokens (ordinals out of
+    range and duplicates no longer count; _apply_visible).  Returns (count, source), or
+    (None, reason) when there is no such view; then amdsmi is tried (its devices' render
+    nodes must be openable too), and nothing else: torch.cuda.device_count() may fall
+    back to hipGetDeviceCount.  `root` (tests: TPT_BENCH_SYSFS_ROOT) prefixes /sys and /dev."""
     root = root if root is not None else os.environ.get("TPT_BENCH_SYSFS_ROOT", "/")
     base = os.path.join(root, "sys/class/kfd/kfd/topology/nodes")
-    n = None
     try:
         nodes = sorted((d for d in os.listdir(base) if d.isdigit()), key=int)
     except OSError:
         nodes = None
+
+    def openable(minor):
+        return os.access(os.path.join(root, "dev/dri/renderD%s" % minor), os.R_OK | os.W_OK)
+
+    devs = []
     if nodes is not None:
-        n = 0
         for nd in nodes:
             props = {}
             try:
@@ -281,15 +326,20 @@ def visible_gpus(root=None):
                 continue
             if int(props.get("simd_count", "0") or 0) <= 0 or "drm_render_minor" not in props:
                 continue  # a CPU node
-            if os.access(os.path.join(root, "dev/dri/renderD%s" % props["drm_render_minor"]), os.R_OK | os.W_OK):
-                n += 1
+            if openable(props["drm_render_minor"]):
+                uid = props.get("unique_id")
+                devs.append({"node": int(nd), "uuid": ("%016x" % int(uid)) if uid and uid.isdigit() and int(uid) else None})
         source = "kfd topology"
     elif root == "/" and not os.environ.get("TPT_BENCH_NO_AMDSMI"):
         try:
             import amdsmi
             amdsmi.amdsmi_init()
             try:
-                n = len(amdsmi.amdsmi_get_processor_handles())
+                for h in amdsmi.amdsmi_get_processor_handles():
+                    e = amdsmi.amdsmi_get_gpu_enumeration_info(h)
+                    if openable(e["drm_render"]):
+                        u = (e.get("hip_uuid") or "")
+                        devs.append({"node": e.get("hsa_id"), "uuid": u[4:] if u.upper().startswith("GPU-") else u or None})
             finally:
                 amdsmi.amdsmi_shut_down()
             source = "amdsmi"
@@ -297,11 +347,15 @@ def visible_gpus(root=None):
             return None, "no kfd topology under %s and amdsmi failed (%s)" % (base, type(e).__name__)
     else:
         return None, "no kfd topology under %s" % base
-    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
-        v = os.environ.get(var)
-        if v is not None:
-            n = min(n, len([x for x in v.split(",") if x.strip()]))
-    return n, source
+    v = os.environ.get("ROCR_VISIBLE_DEVICES")
+    if v is not None:
+        devs = _apply_visible(devs, v)
+    v = os.environ.get("HIP_VISIBLE_DEVICES")
+    if v is None:
+        v = os.environ.get("CUDA_VISIBLE_DEVICES")
+    if v is not None:
+        devs = _apply_visible(devs, v)
+    return len(devs), source
 
 
 def check_distinct(line, world):
@@ -532,7 +586,7 @@ class Runner:
                            "parallelism": "pixel-shard x%d + RCCL reduce" % self.world if self.world > 1
                            else "1 GPU"},
                 "roofline": valu_roofline(tkey, kernel_ms, shard_samples),
-                "roofline_hbm_model": hbm_model(scene, mode, kernel_ms, shard_samples, tkey),
+                "scene_fetch_model": scene_fetch_model(scene, mode, kernel_ms, shard_samples, tkey),
                 "roofline_hbm_measured": hbm_measured(tkey, kernel_ms, shard_samples),
                 "kernel_ms_per_step": round(kernel_ms, 3), "samples_per_rank_step": shard_samples,
                 "nonfinite_pixels": st.nonfinite + st.nonfinite_splat}
@@ -604,6 +658,7 @@ def summary(lines):
         rf, hm = l.get("roofline") or {}, l.get("roofline_hbm_measured") or {}
         out[k] = {"value": l["value"], "ms": l["ms_per_step"], "kernel_ms": l["kernel_ms_per_step"],
                   "valu_frac": rf.get("frac"), "valu_frac_at_isa_rate": rf.get("frac_at_isa_rate"),
+                  "lane_util": rf.get("lane_util"), "valu_frac_lane_weighted": rf.get("frac_lane_weighted"),
                   "hbm_frac_measured": hm.get("frac"),
                   "cpu": (l.get("cpu_baseline") or {}).get("value")}
     return out
@@ -647,7 +702,7 @@ def main():
                    "per-sample seeding: sample j of pixel i seeds tpt_sample_seed(i, j)" if a.sample_seed
                    else "reference seeds pixel+1"),
                "config": head["config"], "roofline": head["roofline"],
-               "roofline_hbm_model": head["roofline_hbm_model"],
+               "scene_fetch_model": head["scene_fetch_model"],
                "roofline_hbm_measured": head["roofline_hbm_measured"], "cpu_baseline": head.get("cpu_baseline"),
                "kernel_ms_per_step": head["kernel_ms_per_step"], "nonfinite_pixels": head["nonfinite_pixels"]}
         for f in ("ranks", "distinct_devices", "kernel_ms_max_over_ranks"):

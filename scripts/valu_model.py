@@ -79,6 +79,33 @@ def kernel_ns(pass_dir, kernel):
     return tot, per
 
 
+def lane_util(pass_dir, kernel):
+    """VALU lane utilisation from a `lane` pass (SQ_THREAD_CYCLES_VALU / (64 x
+    SQ_ACTIVE_INST_VALU), counter_defs.yaml's VALUUtilization): overall and per kernel."""
+    tot, per = counters(pass_dir, kernel)
+    f = lambda c: c["SQ_THREAD_CYCLES_VALU"] / (64.0 * c["SQ_ACTIVE_INST_VALU"])  # noqa: E731
+    ok = lambda c: c.get("SQ_THREAD_CYCLES_VALU") and c.get("SQ_ACTIVE_INST_VALU")  # noqa: E731
+    return (round(f(tot), 4) if ok(tot) else None), {k: round(f(c), 4) for k, c in per.items() if ok(c)}
+
+
+def add_lane(entry, pass_dir, kernel, source):
+    """Lane fields of a valu_model.json entry: lane_util (issue-cycle weighted over the
+    entry's kernels when it has several) and per-kernel lane_util."""
+    overall, per = lane_util(pass_dir, kernel)
+    if overall is None:
+        return entry
+    pk = entry.get("per_kernel", {})
+    w = sum(v.get("issue_cycles_per_launch", 0) * per[k] for k, v in pk.items() if k in per)
+    tw = sum(v.get("issue_cycles_per_launch", 0) for k, v in pk.items() if k in per)
+    for k, v in pk.items():
+        if k in per:
+            v["lane_util"] = per[k]
+    entry["lane_util"] = round(w / tw, 4) if tw else overall
+    entry["lane_util_thread_cycles"] = overall
+    entry["lane_source"] = source
+    return entry
+
+
 def issue_cycles(cnt, cost):
     classes = {k: cnt.get("SQ_INSTS_VALU_" + k, 0.0) for k in CLASSES}
     other = max(0.0, cnt.get("SQ_INSTS_VALU", 0.0) - sum(classes.values()))
@@ -86,7 +113,21 @@ def issue_cycles(cnt, cost):
     return cyc, classes, other
 
 
+def patch_lane(argv):
+    """--patch-lane PROF_DIR KEY WORKLOAD KERNEL SOURCE: add the lane fields of a `lane`
+    pass to an existing entry (a build whose kernels are byte-identical to the entry's)."""
+    prof_dir, key, workload, kernel, source = argv
+    out = os.path.join(ROOT, "profiles", "valu_model.json")
+    db = json.load(open(out))
+    add_lane(db[key], os.path.join(prof_dir, "%s_lane" % workload), kernel, source)
+    json.dump(db, open(out, "w"), indent=1, sort_keys=True)
+    print(key, db[key]["lane_util"], {k: v.get("lane_util") for k, v in db[key].get("per_kernel", {}).items()})
+
+
 def main():
+    import sys
+    if len(sys.argv) > 1 and sys.argv[1] == "--patch-lane":
+        return patch_lane(sys.argv[2:])
     ap = argparse.ArgumentParser()
     ap.add_argument("prof_dir")
     ap.add_argument("key")
@@ -132,6 +173,8 @@ def main():
              "active_inst_valu_quad": cnt.get("SQ_ACTIVE_INST_VALU"), "wave_cycles_quad": cnt.get("SQ_WAVE_CYCLES"),
              "wait_inst_any_quad": cnt.get("SQ_WAIT_INST_ANY"),
              "per_kernel": per, "source": a.source or os.path.relpath(a.prof_dir, ROOT), "note": a.note}
+    if os.path.isdir(p("lane")):
+        add_lane(entry, p("lane"), a.kernel, a.source or os.path.relpath(a.prof_dir, ROOT))
     out = os.path.join(ROOT, "profiles", "valu_model.json")
     db = json.load(open(out)) if os.path.exists(out) else {}
     db[a.key] = entry

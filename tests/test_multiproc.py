@@ -120,7 +120,8 @@ def _fake_sysfs(tmp_path, gpus, cpus=1, openable=None):
     for g in range(gpus):
         (base / str(node)).mkdir(parents=True)
         (base / str(node) / "properties").write_text(
-            "cpu_cores_count 0\nsimd_count 1024\ngfx_target_version 90500\ndrm_render_minor %d\n" % (128 + g))
+            "cpu_cores_count 0\nsimd_count 1024\ngfx_target_version 90500\ndrm_render_minor %d\nunique_id %d\n"
+            % (128 + g, 0x1000 + g))
         if openable is None or g < openable:
             (dri / ("renderD%d" % (128 + g))).write_text("")
         node += 1
@@ -139,6 +140,28 @@ def test_visible_gpus_from_kfd_topology(tmp_path, monkeypatch):
     assert bench.visible_gpus(root)[0] == 2
     n, why = bench.visible_gpus(str(tmp_path / "nowhere"))
     assert n is None and "no kfd topology" in why
+
+
+def test_visible_devices_are_validated(tmp_path, monkeypatch):
+    """a visibility list counts only the devices it names -- duplicates once,
+    and (as HIP / ROCr parse it) nothing from the first ordinal or uuid that names no
+    device on; the levels nest (HIP's ordinals index what ROCr's left)."""
+    import bench
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        monkeypatch.delenv(var, raising=False)
+    root = _fake_sysfs(tmp_path, gpus=4, openable=4)
+    cases = [({"HIP_VISIBLE_DEVICES": "0,0,1"}, 2), ({"HIP_VISIBLE_DEVICES": "0,7,1"}, 1),
+             ({"HIP_VISIBLE_DEVICES": "3,2,1,0"}, 4), ({"HIP_VISIBLE_DEVICES": ""}, 0),
+             ({"CUDA_VISIBLE_DEVICES": "1,x"}, 1), ({"ROCR_VISIBLE_DEVICES": "2,3", "HIP_VISIBLE_DEVICES": "0,1,2"}, 2),
+             ({"ROCR_VISIBLE_DEVICES": "GPU-%016x,GPU-%016x" % (0x1002, 0x1002)}, 1),
+             ({"ROCR_VISIBLE_DEVICES": "GPU-%016x,1" % 0x1003}, 2), ({"ROCR_VISIBLE_DEVICES": "GPU-deadbeef"}, 0),
+             ({"HIP_VISIBLE_DEVICES": "1", "CUDA_VISIBLE_DEVICES": "0,1,2"}, 1)]
+    for env, want in cases:
+        for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+            monkeypatch.delenv(var, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        assert bench.visible_gpus(root) == (want, "kfd topology"), env
 
 
 def test_bench_refuses_more_gpus_than_visible(tmp_path):

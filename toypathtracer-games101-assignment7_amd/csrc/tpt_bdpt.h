@@ -374,12 +374,26 @@ TPT_D int64_t wf_pixel(const WfState& w, int64_t k) { return w.list ? w.list[k] 
 TPT_D int tp_pack(int type, int prim) { return (prim + 1) * 4 + type; }
 TPT_D float4* rec_at(float4* rec, int64_t k, int slot) { return rec + ((k * (2 * kMaxLen) + slot) * kRecV); }
 // Stores of the wavefront state (plain stores, published by the kernel's end).
+// kZ (the walk-scene gen kernel): the record's unused pad zeros are made at the store --
+// hoisted out of gen<2>'s persistent loop as a register quad they were spilled and
+// reloaded at every store (gen<1> keeps the constant form: the opaque one costs it 12
+// B/lane of scratch)
+#ifndef TPT_GEN_REC_Z
+#define TPT_GEN_REC_Z 1
+#endif
+template <bool kZ = false>
 TPT_D void rec_store(const WfState& w, int slot, int64_t k, const BVert& v) {
     float4* r = rec_at(w.rec, k, slot);
     r[0] = make_float4(v.x.x, v.x.y, v.x.z, __builtin_bit_cast(float, tp_pack(v.type, v.prim)));
     r[1] = make_float4(v.N.x, v.N.y, v.N.z, v.pdf);
     r[2] = make_float4(v.alpha.x, v.alpha.y, v.alpha.z, __builtin_bit_cast(float, v.mat));
-    r[3] = make_float4(v.q1, v.q8, 0.0f, 0.0f);
+    if constexpr (kZ) {
+        float z = 0.0f;
+        asm volatile("" : "+v"(z));
+        r[3] = make_float4(v.q1, v.q8, z, z);
+    } else {
+        r[3] = make_float4(v.q1, v.q8, 0.0f, 0.0f);
+    }
 }
 TPT_D void rec_store_q(const WfState& w, int slot, int64_t k, float q1, float q8) {
     *reinterpret_cast<float2*>(rec_at(w.rec, k, slot) + 3) = make_float2(q1, q8);
@@ -612,7 +626,7 @@ TPT_D int gen_step_t(const DScene& s, const WfState& w, int64_t k, int& phase, B
         const float ct = (float)dot3(l0.N, wi);
         sr = safe_div(pdf1, ct);
         ray = make_ray(l0.x, wi);
-        rec_store(w, kMaxLen, k, l0);
+        rec_store<kDefer && TPT_GEN_REC_Z>(w, kMaxLen, k, l0);
         cur = l0;
     } else {
         go = !(i >= kMaxLen - 1 || cur.type == T_BG);
@@ -707,7 +721,7 @@ TPT_D int gen_step_t(const DScene& s, const WfState& w, int64_t k, int& phase, B
         nx.pdf = pdf;
         nx.alpha = v3s(0.0f);  // fresh InternalPathVertex (BDPT.hpp:19)
         if (sr != 0.0f) nx.alpha = safe_div(cur.alpha, sr);
-        rec_store(w, kMaxLen + 1, k, nx);
+        rec_store<kDefer && TPT_GEN_REC_Z>(w, kMaxLen + 1, k, nx);
         prev = cur;
         cur = nx;
         i = 1;
@@ -722,7 +736,7 @@ TPT_D int gen_step_t(const DScene& s, const WfState& w, int64_t k, int& phase, B
     nx.pdf = pdf * rr;
     nx.alpha = divs(cur.alpha * safe_div(bsdf, sr), rr);
     const int base = phase == 0 ? 0 : kMaxLen;
-    rec_store(w, base + i + 1, k, nx);
+    rec_store<kDefer && TPT_GEN_REC_Z>(w, base + i + 1, k, nx);
     // path_rev for j = i - 1: Append(P[j]) after last = P[i], Pre = P[i+1]
     const float rev = append_pdf(s, cur.type, cur.mat, cur.x, cur.N, nx.x, prev.type, prev.x, prev.N);
     rec_store_q(w, base + i - 1, k, safe_div(rev * 1.f, prev.pdf), safe_div(rev * .8f, prev.pdf));

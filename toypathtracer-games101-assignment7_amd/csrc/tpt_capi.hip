@@ -227,7 +227,7 @@ TPT_D void pt_tier(const DScene& s, unsigned char* lds_free, const uint32_t* jt,
         // the wave's shadow-cone mask (pt_cone_mask): the OR of its pixels' masks, with
         // every lane of the wave here; wave-uniform (SGPRs) across the sample loop
         uint64_t cone = ~0ull;
-        if (TPT_PT_CONE && (s.flat & kFlatShadow) && s.nleaf <= 64 && s.n_emitters > 0) {
+        if (TPT_PT_CONE && (s.flat & (kFlatShadow | kFlatNoCone)) == kFlatShadow && s.nleaf <= 64 && s.n_emitters > 0) {
             const uint64_t cm = on && v.type != T_BG ? pt_cone_mask(s, v.x) : 0ull;
             uint32_t lo = (uint32_t)cm, hi = (uint32_t)(cm >> 32);
             for (int o = 1; o < 64; o <<= 1) {
@@ -591,8 +591,8 @@ __global__ __launch_bounds__(kBlock, TPT_GEN_MINWAVES) void tpt_bdpt_gen_kernel(
             camera_vertices(s, wf_pixel(w, k), c0, c1);
         }
         if (!cached) {
-            rec_store(w, 0, it, c0);
-            rec_store(w, 1, it, c1);
+            rec_store<kDef && TPT_GEN_REC_Z>(w, 0, it, c0);
+            rec_store<kDef && TPT_GEN_REC_Z>(w, 1, it, c1);
         }
         prev = c0;
         cur = c1;

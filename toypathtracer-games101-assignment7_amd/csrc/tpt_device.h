@@ -246,7 +246,8 @@ TPT_D Hit traverse_t(const DScene& s, int root, const Ray& r, int cull) {
 // when some lane's box passed.  For scenes with few leaves (the Cornell presets: 32
 // triangles) this beats a per-lane walk; rays with an infinite inv component keep
 // the walk.
-enum { kFlatShadow = 1, kFlatHit = 2, kFlatCompactAll = 4 };  // DScene::flat bits (4: tests force the compacted form)
+enum { kFlatShadow = 1, kFlatHit = 2, kFlatCompactAll = 4, kFlatNoCone = 8 };  // DScene::flat bits (4: tests force the
+// compacted form; 8: tests turn PT's shadow-cone masks off, pt_cone_mask)
 // A walk group (groups[g].b < 0) is a mesh too large for the flat list (the bunny):
 // a lane whose ray passed the group box -- the mesh root's box, tpt_scene.h -- walks
 // the mesh's threaded subtree from the root's right child (a) until kMeshExit, i.e.
