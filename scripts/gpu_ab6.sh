@@ -17,6 +17,6 @@ for i in $(seq 1 $R); do
   for v in "$@"; do
     lib=""; [ "$v" != default ] && lib="TPT_LIB=variants/$v/libtpt.so"
     out=$(env $lib timeout -k 10 300 python bench.py $args --no-cpu 2>/dev/null | tail -1) || { echo "$v failed"; exit 1; }
-    echo "$v $(echo "$out" | python -c "import json,sys; d=json.loads(sys.stdin.read()); s=d.get('shard_model'); print(d.get('ms_per_step'), d.get('kernel_ms_per_step'), json.dumps(s)[:400] if s else '')")" | tee -a gpurun_out/ab6.log
+    echo "$v $(echo "$out" | python -c "import json,sys; d=json.loads(sys.stdin.read()); s=d.get('shard_model'); print(d.get('ms_per_step'), d.get('kernel_ms_per_step'), {k: (v.get('full_kernel_ms'), [(n, v[n].get('eff_kernel'), max(v[n]['kernel_ms'])) for n in ('n2', 'n4', 'n8') if n in v]) for k, v in (s or {}).items() if isinstance(v, dict)})")" | tee -a gpurun_out/ab6.log
   done
 done

@@ -18,10 +18,15 @@ declare -A desc=([pt]="standard PT 1024 spp, --warmup 1 --steps 1 (2 frames)"
 for w in pt bdpt c5 pti c4_ball c4_smooth; do
   [ -d "$p/${w}_kt" ] || continue
   cp "$p/${w}_kt/run_kernel_stats.csv" "profiles/${tag}_${w}_kernel_stats.csv"
-  { echo "# rocprofv3 PMC, $w workload = ${desc[$w]} (scripts/profile_round.sh $tag, build $build); separate passes valu1 / valu2 / misc / fetch / write; values summed over the run's dispatches"
-    for pass in valu1 valu2 misc fetch write; do
+  { echo "# rocprofv3 PMC, $w workload = ${desc[$w]} (scripts/profile_round.sh $tag, build $build); separate passes valu1 / valu2 / misc / fetch / write / lane; values summed over the run's dispatches"
+    for pass in valu1 valu2 misc fetch write lane; do
+      [ -f "$p/${w}_${pass}/run_counter_collection.csv" ] || continue
       python3 scripts/pmc_summary.py "$p/${w}_${pass}/run_counter_collection.csv"
-    done; } > "profiles/${tag}_${w}_pmc.txt"
+    done
+    if [ -f "$p/${w}_lane/run_counter_collection.csv" ]; then
+      echo "# lane utilisation (SQ_THREAD_CYCLES_VALU / (64 x SQ_ACTIVE_INST_VALU)) per kernel:"
+      python3 scripts/pmc_db.py "$p/${w}_lane/run_counter_collection.csv" | grep -E "^ [a-z_]|lane util"
+    fi; } > "profiles/${tag}_${w}_pmc.txt"
 done
 src_of() { echo "profiles/${tag}_$1_pmc.txt, profiles/${tag}_valu_cost.jsonl"; }
 if [ -d "$p/pt_kt" ]; then
