@@ -315,7 +315,10 @@ TPT_D void pt_tier(const DScene& s, unsigned char* lds_free, const uint32_t* jt,
 // dispatched in order, so the short waves of the last tier are what is left to run
 // while the long ones drain: they fill the grid's tail.  A pixel's result does not
 // depend on its tier (the same samples, folded in sample order).
-constexpr int kQT = 64;
+#ifndef TPT_PT_KQT
+#define TPT_PT_KQT 64  // lanes per pixel stream of the tail tier
+#endif
+constexpr int kQT = TPT_PT_KQT;
 template <int kSc, bool kSeeded, int kQP>
 __global__ __launch_bounds__(kBlock, TPT_PT_MINWAVES) void tpt_pt_kernel(DScene s, int spp, int64_t begin,
                                                                         int64_t stride, int64_t count,
@@ -1267,9 +1270,14 @@ int64_t shard_count(int64_t npix, int64_t begin, int64_t stride) {
 // 1173, 10 -> 553 / 1131, 11 -> 556 / 1108, 12 -> 567 / -, 16 -> 585 / -.  Round 3,
 // wavefronts of two iterations: 10 -> 445.0 / 929.5, 11 -> 447.2 / 933.6, 12 -> 449.9 /
 // 932.6 ms.
-#define TPT_GEN_GRID_Q 10  // round 4, four-iteration wavefronts on two gen streams: 8 / 9 / 10 / 11 / 12 ->
-                           // 433.4 / 432.4 / 434.4 / 435.7 / 435.8 ms (Standard BDPT 256 spp); 9 took the
-                           // 1/8 shard from 61.6 to 63.9 ms, so 10 stays
+#define TPT_GEN_GRID_Q 9  // round 4, four-iteration wavefronts on two gen streams: 8 / 9 / 10 / 11 / 12 ->
+                          // 433.4 / 432.4 / 434.4 / 435.7 / 435.8 ms (Standard BDPT 256 spp); 9 took the
+                          // 1/8 shard from 61.6 to 63.9 ms, so 10 stayed.  Round 6 (the faster kernels):
+                          // 9 / 10 / 11 -> 422.2 / 424.5-425.5 / 424.3-425.9 ms whole frame, 1/8 shard
+                          // 61.8 / 60.5 ms: 9 for whole frames, 10 for shards (TPT_GEN_GRID_Q_SHARD)
+#endif
+#ifndef TPT_GEN_GRID_Q_SHARD
+#define TPT_GEN_GRID_Q_SHARD 10  // ... small flat scenes, wavefronts of >= 8 iterations (shards of a frame)
 #endif
 #ifndef TPT_GEN_GRID_Q_WALK
 // ... for scenes with walk groups (the bunny), whose connect runs the walker partition:
@@ -1377,7 +1385,7 @@ int launch_bdpt_chunk(tpt_ctx* c, int spp, int64_t begin, int64_t stride, int64_
     HIP_TRY(c, hipStreamWaitEvent(s2, c->ev_start, 0));
     if (gs[1] != gs[0]) HIP_TRY(c, hipStreamWaitEvent(gs[1], c->ev_start, 0));
     const unsigned pblocks = (unsigned)((count + kBlock - 1) / kBlock);
-    const int gen_q = c->sc != 2 ? TPT_GEN_GRID_Q
+    const int gen_q = c->sc != 2 ? (nb >= 8 ? TPT_GEN_GRID_Q_SHARD : TPT_GEN_GRID_Q)
                       : !two_gen  ? TPT_GEN_GRID_Q_WALK
                       : nb >= 8   ? TPT_GEN_GRID_Q_WALK_SHARD
                                   : TPT_GEN_GRID_Q_WALK2;
