@@ -424,7 +424,9 @@ TPT_D void rec_store_q(const WfState& w, int slot, int64_t k, float q1, float q8
 #define TPT_GEN_DEFER 1
 #endif
 #ifndef TPT_GEN_DEFER_MIN
-#define TPT_GEN_DEFER_MIN 24  // lanes wanting a walk before a wave walks
+#define TPT_GEN_DEFER_MIN 12  // lanes wanting a walk before a wave walks (round 6, with the stealing walks and
+                              // the compiler changes, bunny 256 spp 24 / 20 / 16 / 12 / 8 -> 624.4 / 619.1 /
+                              // 617.0 / 616.3 / 619.5 ms, 1/8 shard 93.2 / 92.6 / 91.8 / 91.6 / 91.0 ms)
 #endif
 #ifndef TPT_GEN_DEFER_MAX
 #define TPT_GEN_DEFER_MAX 3  // iterations a parked lane waits at most
