@@ -128,8 +128,11 @@ TPT_D bool shadow_v(const DScene& s, const BVert& v1, const BVert& v2) {
 // kCls >= 0: the caller's strategies are all of one task class (tpt_bdpt_scatter_kernel's
 // runs: 0 s = 0, 1 t > 1 and s > 1, 2 t > 1 and s = 1, 3 t = 1), so the branches of the
 // other classes fold away (the same float ops in the same order for the strategies run).
-template <int kCls = -1, class P>
-TPT_D V3 path_weight(const DScene& s, const P& paths, int sl, int tl) {
+// kDS: the shadow query is not made here; *need is set when the strategy needs it (a
+// non-zero unshadowed contribution with sl != 0) and the caller makes it (the queued
+// connect, tpt_capi.hip): the result is then this value or 0.
+template <int kCls = -1, bool kDS = false, class P>
+TPT_D V3 path_weight(const DScene& s, const P& paths, int sl, int tl, bool* need = nullptr) {
     if constexpr (kCls == 0) __builtin_assume(sl == 0 && tl >= 2);
     if constexpr (kCls == 1) __builtin_assume(sl >= 2 && tl >= 2);
     if constexpr (kCls == 2) __builtin_assume(sl == 1 && tl >= 2);
@@ -223,7 +226,11 @@ TPT_D V3 path_weight(const DScene& s, const P& paths, int sl, int tl) {
 #ifndef TPT_DIAG_NO_CONN_SHADOW
 #define TPT_DIAG_NO_CONN_SHADOW 0  // diagnostics builds only (timing attribution; wrong images)
 #endif
-        if (!TPT_DIAG_NO_CONN_SHADOW && shadow_v(s, cz, ly)) return v3s(0.0f);
+        if constexpr (kDS) {
+            *need = true;
+        } else {
+            if (!TPT_DIAG_NO_CONN_SHADOW && shadow_v(s, cz, ly)) return v3s(0.0f);
+        }
     }
     return res;
 }
@@ -592,6 +599,9 @@ TPT_D Hit walk4_steal(const DScene& s, int root, bool need, Ray r, int cl, const
 // walking in them, [3] wave-ticks inside whole gen steps, [4] steps (100 MHz ticks)
 __device__ unsigned long long tpt_walkstat[8];
 #endif
+#ifndef TPT_GEN_MERGE
+#define TPT_GEN_MERGE 1  // one call site for both phases' cosine-weighted samples (gen_step_t)
+#endif
 // One generation step (see the comment above gen_step's callers).  Returns 1 when the
 // subpath continues, 0 when it has ended (its vertex count is then i + 1), 2 when the
 // step was deferred (kDefer only; `pend` counts the iterations it has waited).
@@ -613,6 +623,80 @@ TPT_D int gen_step_t(const DScene& s, const WfState& w, int64_t k, int& phase, B
         best.prim = __float_as_int(dl.at(kGdPrim));
         best.dist = __hiloint2double(__float_as_int(dl.at(kGdDhi)), __float_as_int(dl.at(kGdDlo)));
         ray = make_ray(cur.x, v3(dl.at(kGdDx), dl.at(kGdDy), dl.at(kGdDz)));  // the same Ray as when parked
+    } else if (TPT_GEN_MERGE) {
+        // Both phases' cosine-weighted samples in ONE call site (round 6): the light start's
+        // (GenerateLightPath, BDPT.cpp:61-90) and the Dieletric extension's diffuse branch
+        // (Material::sample, Material.cpp:150-214).  In a wave of persistent lanes both
+        // kinds are nearly always present, and as two call sites the f64 sin/cos ran twice
+        // per step with a few lanes each.  Per lane the same draws in the same order (the
+        // light sample's three, or the GGX pair and the coin, before the cosine pair) and
+        // the same float operations; only the SIMD schedule changes.
+        BVert l0;
+        V3 wo = v3s(0.0f), wi = v3s(0.0f), H = v3s(0.0f);
+        float pdfv = 0.0f;
+        Shade csh;
+        bool wantc = false, diel = false, spec = false;
+        float rough = 0.0f;
+        if (start) {
+            const DObj lo = s.objs[s.emitters[0]];
+            V3 pc, pn;
+            int pp;
+            object_sample(s, lo, pc, pn, pp, rs);
+            l0.x = pc; l0.N = pn; l0.type = T_LIGHT; l0.prim = pp; l0.mat = lo.mat;
+            l0.pdf = lo.pdf;
+            l0.alpha = divs(load_mat(s, lo.mat).em, l0.pdf);
+            l0.q1 = l0.q8 = 0.0f;
+            csh = make_shade(pn, pn);
+            wantc = true;
+        } else {
+            go = !(i >= kMaxLen - 1 || cur.type == T_BG);
+            if (go) {
+                wo = normalized(prev.x - cur.x);
+                const Mat m = load_mat(s, cur.mat);
+                if (m.type == TPT_DIELETRIC) {
+                    diel = true;
+                    rough = m.rough;
+                    csh = make_shade(cur.N, wo);
+                    const float d1 = rng_float(rs), d2 = rng_float(rs);
+                    spec = xorshift32(rs) < kCoinHalf;  // rng_float(rs) < 0.5f
+                    if (spec) {
+                        H = ggx_h(csh, rough, d1, d2);
+                        wi = reflect(wo, H);
+                    } else {
+                        wantc = true;
+                    }
+                } else {
+                    wi = mat_sample<true>(m, wo, cur.N, &pdfv, rs);
+                }
+            }
+        }
+        float pdc = 0.0f;
+        if (wantc) wi = cosine_sample(csh, pdc, rs);
+        if (start) {
+            const float ct = (float)dot3(l0.N, wi);
+            sr = safe_div(pdc, ct);
+            ray = make_ray(l0.x, wi);
+            rec_store<kDefer && TPT_GEN_REC_Z>(w, kMaxLen, k, l0);
+            cur = l0;
+        } else if (go) {
+            if (diel) {  // Material::sample's Dieletric tail, either branch (mat_sample<true>)
+                const V3 n = csh.n;
+                if (!spec) H = normalized(wi + wo);
+                const float pdf_h = ggx_half_pdf(n, H, rough);
+                const float jr = safe_div(1.0f, 4.0f * fabs_((float)dot3(wo, H)));
+                const float pd = spec ? cosine_pdf(n, wi) : pdc;
+                pdfv = (pdf_h * jr + pd) * 0.5f;
+                if ((double)csh.nv * dot3(wi, n) < 0.0f) pdfv = 0.0f;
+            }
+            const float rr = i > 4 ? .8f : 1.f;
+            go = !(rng_float(rs) > rr);
+            if (go) {
+                const float ct = (float)dabs_(dot3(cur.N, wi));
+                sr = safe_div(pdfv, ct);
+                ray = make_ray(cur.x, wi);
+                cl = dot3(cur.N, wi) > 0.0f ? TPT_CULL_BACK : TPT_CULL_FRONT;
+            }
+        }
     } else if (start) {
         const DObj lo = s.objs[s.emitters[0]];
         V3 pc, pn;

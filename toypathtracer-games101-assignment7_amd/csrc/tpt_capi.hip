@@ -799,6 +799,98 @@ TPT_D void conn_task(const DScene& s, const WfState& w, float* __restrict__ spla
         if (splat) splat_wave(s, sp, lx, eye, v, splat);
 }
 
+// Queued shadow queries (round 6, TPT_CONN_QUEUE).  A strategy's shadow query
+// (BDPT.cpp:205) is needed only when its unshadowed contribution is not 0, so in a wave of
+// 64 strategies only some lanes make it, and the others idle through it (for walk-group
+// scenes: through the bunny walks).  Here PathWeight runs without it (path_weight<.., kDS>)
+// and stores the unshadowed result at the task's index; the tasks that need the query go
+// into a per-wave LDS queue, and the queries run 64 at a time, dense: a shadowed
+// strategy's result is overwritten with 0 (t > 1) or its splat is dropped (t = 1; the
+// splat is added only after the query, from the stored value).  Same queries on the
+// same vertices, same results; splats are fp32 atomics in another order.
+#ifndef TPT_CONN_QUEUE
+#define TPT_CONN_QUEUE 1  // small flat scenes, wavefronts of < 8 iterations (whole frames): Standard BDPT 256 spp
+                          // 423.5-425.2 -> 414.7-417.1 ms same-box; its 1/8 shard 60.3 -> 60.7 ms, so shards keep
+                          // the in-place queries.  Walk-group scenes keep them too (bunny 256 spp -0.5 %, and this
+                          // compiler crashed building the partitioned kernel with the queue and the AMDGPU trackers)
+#endif
+constexpr int kShQ = 128;  // per-wave queue slots (<= 63 left over + 64 appended)
+struct ShadowQueue {
+    uint32_t* q;  // this wave's kShQ task indices (LDS)
+    int n;        // queued (wave-uniform)
+};
+// PathWeight of task g without the shadow query; true when the query is needed.
+TPT_D bool conn_unshadowed(const DScene& s, const WfState& w, int64_t g, bool on) {
+    bool need = false;
+    if (on) {
+        const unsigned tk = w.task[g];
+        const int64_t k = (int64_t)(tk & kTaskPixelMask);
+        const int t = (int)((tk >> 22) & 31), sl = (int)(tk >> 27);
+        GlobPaths P;
+        P.rec = rec_at(w.rec, k, 0);
+        const V3 v = vmax0(path_weight<-1, true>(s, P, sl, t, &need));
+        w.res[3 * g] = v.x;
+        w.res[3 * g + 1] = v.y;
+        w.res[3 * g + 2] = v.z;
+    }
+    return need;
+}
+// The queries of queue entries [0, cnt) (cnt <= 64, lane i takes entry i); every lane of
+// the wave calls it.
+TPT_D void conn_shadow_round(const DScene& s, const WfState& w, float* __restrict__ splat, const uint32_t* q, int cnt,
+                             V3 eye) {
+    const int lane = (int)lane_id();
+    bool want = false;
+    V3 v = v3s(0.0f), lx = eye;
+    if (lane < cnt) {
+        const int64_t g = (int64_t)q[lane];
+        const unsigned tk = w.task[g];
+        const int64_t k = (int64_t)(tk & kTaskPixelMask);
+        const int t = (int)((tk >> 22) & 31), sl = (int)(tk >> 27);
+        GlobPaths P;
+        P.rec = rec_at(w.rec, k, 0);
+        const BVert cz = P.cam(t - 1), ly = P.lit(sl - 1);
+        const bool sh = !TPT_DIAG_NO_CONN_SHADOW && shadow_v(s, cz, ly);
+        if (t > 1) {
+            if (sh) {
+                w.res[3 * g] = 0.0f;
+                w.res[3 * g + 1] = 0.0f;
+                w.res[3 * g + 2] = 0.0f;
+            }
+        } else if (splat && !sh) {
+            want = true;
+            lx = ly.x;
+            v = v3(w.res[3 * g], w.res[3 * g + 1], w.res[3 * g + 2]);
+        }
+    }
+    if (splat) splat_wave(s, want, lx, eye, v, splat);
+}
+// Append this round's needing lanes (task g) and run the full rounds of 64.
+TPT_D void conn_queue_push(const DScene& s, const WfState& w, float* __restrict__ splat, ShadowQueue& sq, bool need,
+                           int64_t g, V3 eye) {
+    const uint64_t m = __ballot(need);
+    if (need) sq.q[sq.n + mbcnt64(m)] = (uint32_t)g;
+    sq.n += __popcll(m);
+    wave_lds_sync();
+    if (sq.n >= 64) {
+        conn_shadow_round(s, w, splat, sq.q, 64, eye);
+        wave_lds_sync();
+        const int lane = (int)lane_id();
+        const uint32_t rest = lane + 64 < sq.n ? sq.q[lane + 64] : 0u;
+        wave_lds_sync();
+        if (lane + 64 < sq.n) sq.q[lane] = rest;
+        sq.n -= 64;
+        wave_lds_sync();
+    }
+}
+TPT_D void conn_queue_flush(const DScene& s, const WfState& w, float* __restrict__ splat, ShadowQueue& sq, V3 eye) {
+    if (sq.n > 0) {
+        conn_shadow_round(s, w, splat, sq.q, sq.n, eye);
+        sq.n = 0;
+        wave_lds_sync();
+    }
+}
+
 // Walker partition (round 4).  For a scene with walk groups the shadow query of a
 // strategy (BDPT.cpp:205), from the camera-side vertex toward the light-side one,
 // walks the mesh's tree when its ray passes the walk group's box; dealt pixel-major,
@@ -842,7 +934,7 @@ TPT_D bool conn_marked(const DScene& s, const WfState& w, int64_t g, int gi) {
 
 // One lane per strategy, grid-stride in wave-sized steps so that every lane of a
 // wave stays in the loop until the wave is done (splat_wave needs the whole wave).
-template <int kSc>
+template <int kSc, bool kQueue = false>
 __global__ __launch_bounds__(kBlock, TPT_CONN_MINWAVES) void tpt_bdpt_conn_kernel(DScene s, WfState w, float* __restrict__ splat) {
     stage_scene<kSc>(s);
     __shared__ QScratch qsm[kBlock / 64];
@@ -855,7 +947,16 @@ __global__ __launch_bounds__(kBlock, TPT_CONN_MINWAVES) void tpt_bdpt_conn_kerne
     const int64_t total = total_tasks(w);
     const V3 eye = v3(s.eye[0], s.eye[1], s.eye[2]);
     constexpr bool kPart = TPT_CONN_SORT == 2 || (TPT_CONN_SORT == 1 && kSc == 2);
-    if constexpr (!kPart) {
+    if constexpr (!kPart && kQueue) {  // queued shadow queries (small flat scenes, whole frames)
+        __shared__ uint32_t shq_all[kBlock / 64][kShQ];
+        ShadowQueue sq{shq_all[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)], 0};
+        for (int64_t g0 = (int64_t)blockIdx.x * kBlock + (threadIdx.x & ~63); g0 < total;
+             g0 += (int64_t)gridDim.x * kBlock) {
+            const int64_t g = g0 + lane_id();
+            conn_queue_push(s, w, splat, sq, conn_unshadowed(s, w, g, g < total), g, eye);
+        }
+        conn_queue_flush(s, w, splat, sq, eye);
+    } else if constexpr (!kPart) {
         for (int64_t g0 = (int64_t)blockIdx.x * kBlock + (threadIdx.x & ~63); g0 < total;
              g0 += (int64_t)gridDim.x * kBlock) {
             const int64_t g = g0 + lane_id();
@@ -1392,7 +1493,10 @@ int launch_bdpt_chunk(tpt_ctx* c, int spp, int64_t begin, int64_t stride, int64_
     // persistent gen grid: as many workgroups as are resident at once, a multiple of
     // the 8 queue shards, and no more than the pixels need
     const auto gen_k = c->sc == 2 ? tpt_bdpt_gen_kernel<2> : c->sc == 1 ? tpt_bdpt_gen_kernel<1> : tpt_bdpt_gen_kernel<0>;
-    const auto conn_k = c->sc == 2 ? tpt_bdpt_conn_kernel<2> : c->sc == 1 ? tpt_bdpt_conn_kernel<1> : tpt_bdpt_conn_kernel<0>;
+    const bool qconn = TPT_CONN_QUEUE && nb < 8;
+    const auto conn_k = c->sc == 2 ? tpt_bdpt_conn_kernel<2>
+                        : c->sc == 1 ? (qconn ? tpt_bdpt_conn_kernel<1, true> : tpt_bdpt_conn_kernel<1>)
+                                     : (qconn ? tpt_bdpt_conn_kernel<0, true> : tpt_bdpt_conn_kernel<0>);
     int per_cu = 0;
     HIP_TRY(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(
                    &per_cu, (const void*)gen_k, kBlock, shmem));

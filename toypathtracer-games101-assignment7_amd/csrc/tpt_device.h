@@ -1293,6 +1293,9 @@ TPT_D void bsdf_pdf(const Mat& m, V3 wo, V3 wi, V3 N, V3& f_out, float& pdf_out)
 // Material::sample (Material.cpp:150-214).  kLateH (BDPT's gen; PT measured 0.8 %
 // slower with it, 43.55 vs 43.2 ms): the Dieletric branch makes its GGX half vector
 // after the coin.
+#ifndef TPT_MAT_TAIL_MERGE
+#define TPT_MAT_TAIL_MERGE 1
+#endif
 template <bool kLateH = false>
 TPT_D V3 mat_sample(const Mat& m, V3 wo, const Shade& sh, float* pdf, uint32_t& rs) {
     const V3 n = sh.n;
@@ -1322,6 +1325,27 @@ TPT_D V3 mat_sample(const Mat& m, V3 wo, const Shade& sh, float* pdf, uint32_t& 
         *pdf = (pdf_h * jr + pd) * 0.5f;
         if ((double)sh.nv * dot3(wid, n) < 0.0f) *pdf = 0.0f;
         return wid;
+    }
+    if (TPT_MAT_TAIL_MERGE && m.type == TPT_DIELETRIC) {
+        // (round 6) the half vector first (its two draws, then the coin: the reference's
+        // order), each branch makes only its direction, and the pdf tail that both
+        // branches share -- the GGX half-vector pdf, the Jacobian, the mix -- runs once
+        // for the wave instead of once per branch; per lane the same float ops as below
+        V3 H = ggx_sample_h(sh, m.rough, rs);
+        V3 wi;
+        float pd;
+        if (xorshift32(rs) < kCoinHalf) {  // rng_float(rs) < 0.5f
+            wi = reflect(wo, H);
+            pd = cosine_pdf(n, wi);
+        } else {
+            wi = cosine_sample(sh, pd, rs);
+            H = normalized(wi + wo);
+        }
+        const float pdf_h = ggx_half_pdf(n, H, m.rough);
+        const float jr = safe_div(1.0f, 4.0f * fabs_((float)dot3(wo, H)));
+        *pdf = (pdf_h * jr + pd) * 0.5f;
+        if ((double)sh.nv * dot3(wi, n) < 0.0f) *pdf = 0.0f;
+        return wi;
     }
     V3 H = ggx_sample_h(sh, m.rough, rs);
     V3 wis = reflect(wo, H);
