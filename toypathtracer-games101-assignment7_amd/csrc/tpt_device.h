@@ -1294,9 +1294,10 @@ TPT_D void bsdf_pdf(const Mat& m, V3 wo, V3 wi, V3 N, V3& f_out, float& pdf_out)
 // slower with it, 43.55 vs 43.2 ms): the Dieletric branch makes its GGX half vector
 // after the coin.
 #ifndef TPT_MAT_TAIL_MERGE
-#define TPT_MAT_TAIL_MERGE 1
+#define TPT_MAT_TAIL_MERGE 1  // Dieletric pdf tail once per wave (PT: 40.35-40.57 -> 39.50-39.66 ms, configs[3] -2.2 %
+                              // same-box; PT-indirect keeps the branch form, 553 vs 574 ms)
 #endif
-template <bool kLateH = false>
+template <bool kLateH = false, bool kTail = TPT_MAT_TAIL_MERGE>
 TPT_D V3 mat_sample(const Mat& m, V3 wo, const Shade& sh, float* pdf, uint32_t& rs) {
     const V3 n = sh.n;
     if (kLateH && m.type == TPT_DIELETRIC) {
@@ -1326,7 +1327,7 @@ TPT_D V3 mat_sample(const Mat& m, V3 wo, const Shade& sh, float* pdf, uint32_t& 
         if ((double)sh.nv * dot3(wid, n) < 0.0f) *pdf = 0.0f;
         return wid;
     }
-    if (TPT_MAT_TAIL_MERGE && m.type == TPT_DIELETRIC) {
+    if (kTail && m.type == TPT_DIELETRIC) {
         // (round 6) the half vector first (its two draws, then the coin: the reference's
         // order), each branch makes only its direction, and the pdf tail that both
         // branches share -- the GGX half-vector pdf, the Jacobian, the mix -- runs once
@@ -1666,7 +1667,7 @@ TPT_D bool pti_step(const DScene& s, const PTV& v, PtiPath& p, uint32_t& rs) {
     const V3 x = v.x, wo = -p.r.d;
     const Shade sh = make_shade(v.N, wo);
     float pdf_b;
-    const V3 wib = mat_sample(m, wo, sh, &pdf_b, rs);  // :76
+    const V3 wib = mat_sample<false, false>(m, wo, sh, &pdf_b, rs);  // :76 (the per-branch form: faster here)
     for (int li = 0; li < s.n_emitters; ++li) {        // :82-106, as pt_sample
         const DObj o = s.objs[s.emitters[li]];
         V3 pc, pn;
