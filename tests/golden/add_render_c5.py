@@ -1,0 +1,54 @@
+"""Add the real Renderer::Render route to tests/golden/frame_c5.npz (configs[4], bunny
+BDPT at its own 4096 spp; VERDICT r5 Missing #3).  Data only: no reference source is
+copied.
+
+    nice python tests/golden/add_render_c5.py        (~2-3 h of the container's 8 cores)
+
+frame_c5.npz was made through the per-pixel route alone (make_frames.py TRACE_ONLY): the
+radiance and the t = 1 splat buffer of ref_trace_pixels.  This renders the same frame with
+the real Renderer::Render (Renderer.cpp:68-127: 8 std::async workers, each with its own splat
+buffer, merged at Renderer.cpp:98-114), stores its render_blocks / render_crops beside the
+existing summaries, and checks the two routes against each other first: 8x8 block means are
+linear, so Render's blocks must equal rgb_blocks + splat_blocks up to the splat buffers'
+summation order (relative L2 < 1e-5 over the finite blocks, as make_frames.py asks of the
+whole frames).  The trace_only flag is then dropped, so test_bdpt_frame[c5] also checks the
+GPU's radiance + splats against Render."""
+import os
+import sys
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(HERE))
+import make_frames  # noqa: E402
+from oracle_bind import Reference, ref_available  # noqa: E402
+
+
+def main():
+    if not ref_available():
+        sys.exit("oracle/_ref/libref.so missing: run oracle/build_ref.sh first")
+    path = os.path.join(HERE, "frame_c5.npz")
+    g = dict(np.load(path))
+    assert str(g["preset"]) == "bunny" and int(g["mode"]) == 1 and int(g["spp"]) == 4096
+    t0 = time.time()
+    render = Reference("bunny").render(1, 4096, threads=make_frames.WORKERS)
+    print("Renderer::Render, bunny BDPT 4096 spp, %d workers: %.0f s" % (make_frames.WORKERS, time.time() - t0),
+          flush=True)
+    rb = make_frames.frame_blocks(render, "render")
+    a = rb["render_blocks"].astype(np.float64)
+    b = g["rgb_blocks"].astype(np.float64) + g["splat_blocks"].astype(np.float64)
+    fin = np.isfinite(a).all(-1) & np.isfinite(b).all(-1)
+    rel = np.linalg.norm(a[fin] - b[fin]) / np.linalg.norm(a[fin])
+    print("Render blocks vs radiance + splat blocks: relL2 %.3g over %d finite blocks (of %d)" %
+          (rel, int(fin.sum()), fin.size), flush=True)
+    assert rel < 1e-5, rel
+    g.update(rb)
+    g["render_vs_trace_relL2"] = np.float64(rel)
+    g.pop("trace_only", None)
+    np.savez_compressed(path, **g)
+    print("frame_c5.npz: render route added in %.0f s" % (time.time() - t0), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -814,6 +814,10 @@ TPT_D void conn_task(const DScene& s, const WfState& w, float* __restrict__ spla
                           // the in-place queries.  Walk-group scenes keep them too (bunny 256 spp -0.5 %, and this
                           // compiler crashed building the partitioned kernel with the queue and the AMDGPU trackers)
 #endif
+#ifndef TPT_CONN_QUEUE_WALK
+#define TPT_CONN_QUEUE_WALK 0  // walk-group scenes: the queue behind the walker partition (OFF: bunny 256 spp
+                               // 609.1-610.4 -> 610.1-614.3 ms same-box, c5 pins green)
+#endif
 constexpr int kShQ = 128;  // per-wave queue slots (<= 63 left over + 64 appended)
 struct ShadowQueue {
     uint32_t* q;  // this wave's kShQ task indices (LDS)
@@ -966,6 +970,8 @@ __global__ __launch_bounds__(kBlock, TPT_CONN_MINWAVES) void tpt_bdpt_conn_kerne
         __shared__ uint16_t srt_all[kBlock / 64][kSortN];
         const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
         uint16_t* srt = srt_all[wv];
+        __shared__ uint32_t shq_p[kQueue ? kBlock / 64 : 1][kQueue ? kShQ : 1];
+        ShadowQueue sq{shq_p[kQueue ? wv : 0], 0};
         int box = -1;  // the first walk group
         for (int gi = s.ngroup - 1; gi >= 0; --gi)
             if (s.groups[gi].b < 0) box = gi;
@@ -991,10 +997,12 @@ __global__ __launch_bounds__(kBlock, TPT_CONN_MINWAVES) void tpt_bdpt_conn_kerne
             wave_lds_sync();
             for (int j0 = 0; j0 < kSortN; j0 += 64) {
                 const int64_t g = c0 + (int64_t)srt[j0 + lane_id()];
-                conn_task(s, w, splat, g, g < total, eye);
+                if constexpr (kQueue) conn_queue_push(s, w, splat, sq, conn_unshadowed(s, w, g, g < total), g, eye);
+                else conn_task(s, w, splat, g, g < total, eye);
             }
             wave_lds_sync();  // the next chunk reuses srt
         }
+        if constexpr (kQueue) conn_queue_flush(s, w, splat, sq, eye);
     }
 }
 
@@ -1494,7 +1502,7 @@ int launch_bdpt_chunk(tpt_ctx* c, int spp, int64_t begin, int64_t stride, int64_
     // the 8 queue shards, and no more than the pixels need
     const auto gen_k = c->sc == 2 ? tpt_bdpt_gen_kernel<2> : c->sc == 1 ? tpt_bdpt_gen_kernel<1> : tpt_bdpt_gen_kernel<0>;
     const bool qconn = TPT_CONN_QUEUE && nb < 8;
-    const auto conn_k = c->sc == 2 ? tpt_bdpt_conn_kernel<2>
+    const auto conn_k = c->sc == 2 ? tpt_bdpt_conn_kernel<2, TPT_CONN_QUEUE_WALK != 0>
                         : c->sc == 1 ? (qconn ? tpt_bdpt_conn_kernel<1, true> : tpt_bdpt_conn_kernel<1>)
                                      : (qconn ? tpt_bdpt_conn_kernel<0, true> : tpt_bdpt_conn_kernel<0>);
     int per_cu = 0;
