@@ -15,6 +15,8 @@ trk="-mllvm -amdgpu-use-amdgpu-trackers=1"
 [ "${TRACKERS:-1}" = 0 ] && trk=""  # TRACKERS=0: without the AMDGPU trackers (the Makefile's default has them)
 /opt/rocm/bin/hipcc -std=c++17 -O3 -fPIC -ffp-contract=off -Wno-unused-function --offload-arch=gfx950 \
     -munsafe-fp-atomics -fno-slp-vectorize $trk "$@" -c -o "$out/tpt_capi.o" "$pkg/csrc/tpt_capi.hip"
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o "$out/libtpt.so" "$out/tpt_capi.o" \
+/opt/rocm/bin/hipcc -std=c++17 -O3 -fPIC -ffp-contract=off -Wno-unused-function --offload-arch=gfx950 \
+    -munsafe-fp-atomics -fno-slp-vectorize "$@" -c -o "$out/tpt_conn2.o" "$pkg/csrc/tpt_conn2.hip"  # no trackers (Makefile)
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o "$out/libtpt.so" "$out/tpt_capi.o" "$out/tpt_conn2.o" \
     "$out/tpt_scene_build.o" "$pkg/build/tpt_multi.o" "$pkg/build/scene_api.o" "$pkg/build/film.o" -ldl
 echo "built $out/libtpt.so ($*)"

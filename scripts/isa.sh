@@ -1,5 +1,7 @@
 #!/usr/bin/env bash
-# Device assembly of the kernel TU (with line tables) + spill counts per kernel.
+# Device assembly of the kernel TU (with line tables) + spill counts per kernel.  (The
+# walk-group scenes' connect kernel is in csrc/tpt_conn2.hip, built without the trackers:
+# run with TRACKERS=0 and -DTPT_TU_CONN2=1 on that file for it.)
 #   scripts/isa.sh OUT.s [extra hipcc flags...]
 set -eu
 out=$1; shift

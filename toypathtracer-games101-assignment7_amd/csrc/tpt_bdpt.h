@@ -597,7 +597,7 @@ TPT_D Hit walk4_steal(const DScene& s, int root, bool need, Ray r, int cl, const
 #if TPT_GEN_STATS
 // diagnostics only: [0] wave-ticks inside deferred-step walks, [1] such walks, [2] lanes
 // walking in them, [3] wave-ticks inside whole gen steps, [4] steps (100 MHz ticks)
-__device__ unsigned long long tpt_walkstat[8];
+TPT_TU_STATIC __device__ unsigned long long tpt_walkstat[8];
 #endif
 #ifndef TPT_GEN_MERGE
 #define TPT_GEN_MERGE 1  // one call site for both phases' cosine-weighted samples (gen_step_t)

@@ -202,7 +202,7 @@ TPT_D void fold_dpp(V3& acc, V3 L, int n) {
 #endif
 #if TPT_PT_WAVETIME
 constexpr int kWaveTimeMax = 1 << 17;
-__device__ unsigned long long tpt_wavetime[3 * kWaveTimeMax];  // start, end, hw id per wave
+TPT_TU_STATIC __device__ unsigned long long tpt_wavetime[3 * kWaveTimeMax];  // start, end, hw id per wave
 #endif
 
 // kSeeded: TPT_FLAG_SAMPLE_SEED -- each sample seeds its own stream (sample_seed), so
@@ -465,8 +465,8 @@ __global__ __launch_bounds__(kBlock, TPT_PTI_MINWAVES) void tpt_pti_kernel(DScen
 constexpr int kGenStatMax = 1 << 16;
 // per wave: kernel (0: gen) | launch ordinal << 8, step iterations, lane-steps, idle
 // iterations, real-time ticks (100 MHz)
-__device__ unsigned long long tpt_genstats[5 * kGenStatMax];
-__device__ unsigned tpt_genstat_n;
+TPT_TU_STATIC __device__ unsigned long long tpt_genstats[5 * kGenStatMax];
+TPT_TU_STATIC __device__ unsigned tpt_genstat_n;
 struct GenStat {
     unsigned long long it = 0, ls = 0, idle = 0, t0 = 0;
     TPT_D void begin() { t0 = __builtin_amdgcn_s_memrealtime(); }
@@ -755,6 +755,7 @@ TPT_D int64_t total_tasks(const WfState& w) {
     return (int64_t)(t1 & 0xffffffffull) + (int64_t)(t1 >> 32) + (int64_t)(t2 & 0xffffffffull) + (int64_t)(t2 >> 32);
 }
 
+#if !TPT_TU_CONN2
 __global__ __launch_bounds__(kBlock) void tpt_bdpt_scatter_kernel(WfState w, unsigned* __restrict__ queue) {
     const int64_t k = (int64_t)blockIdx.x * kBlock + threadIdx.x;  // item
     if (k < 8) queue[k * 16] = 0;  // gen of the next wavefront (same stream, after this kernel) starts its shards at 0
@@ -771,6 +772,7 @@ __global__ __launch_bounds__(kBlock) void tpt_bdpt_scatter_kernel(WfState w, uns
         for (int sl = 2; sl <= ln; ++sl) w.task[g1 + sl] = kt | (unsigned)sl << 27;
     }
 }
+#endif
 
 // One strategy (task g) of connect: PathWeight, the result at its task index (t > 1)
 // or the splat of the wave (t = 1; call with every lane of the wave).
@@ -1005,6 +1007,13 @@ __global__ __launch_bounds__(kBlock, TPT_CONN_MINWAVES) void tpt_bdpt_conn_kerne
         if constexpr (kQueue) conn_queue_flush(s, w, splat, sq, eye);
     }
 }
+
+// The walk-group scenes' connect (kSc = 2) is compiled in tpt_conn2.hip, without the
+// AMDGPU register-pressure trackers: with them this compiler segfaults in its machine
+// scheduler on that kernel for some code shapes (round 6: the queued walker partition,
+// the uncapped connect stealing), and the bunny measures the same without them.
+extern template __global__ void tpt_bdpt_conn_kernel<2, TPT_CONN_QUEUE_WALK != 0>(DScene, WfState, float*);
+#if !TPT_TU_CONN2
 
 // Class kernels (round 6, TPT_CONN_CLASS, small flat scenes; OFF: measured slower).  The
 // emission-only run (s = 0: no connection, no shadow query, one MIS chain) needs 58
@@ -2041,3 +2050,4 @@ int tpt_intersect(tpt_ctx* c, const float* rays, int64_t n, int32_t cull, float*
 }
 
 }  // extern "C"
+#endif  // !TPT_TU_CONN2

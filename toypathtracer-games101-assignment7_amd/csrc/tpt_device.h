@@ -18,6 +18,13 @@
 namespace tpt {
 
 #define TPT_D __device__ __forceinline__
+// tpt_conn2.hip compiles tpt_capi.hip's walk-scene connect kernel alone (TPT_TU_CONN2): its
+// device globals get internal linkage there, so the two objects link side by side
+#if defined(TPT_TU_CONN2) && TPT_TU_CONN2
+#define TPT_TU_STATIC static
+#else
+#define TPT_TU_STATIC
+#endif
 
 constexpr int kBlock = 256;     // threads per workgroup (4 waves)
 // ------------------------------------------------------------------ rays --
@@ -674,7 +681,12 @@ TPT_D Hit traverse_flat_c(const DScene& s, const Ray& r, int cull) {
 // owner's ray.  Any hit below the owner's threshold marks the owner shadowed; its other
 // jobs then end.  The answer is the any-hit answer, so the order of the jobs is free.
 #ifndef TPT_CONN_STEAL
-#define TPT_CONN_STEAL 0
+#define TPT_CONN_STEAL 1  // round 6, with the compiler changes: bunny BDPT 256 spp 609.3-611.7 -> 600.4-601.6 ms
+                          // same-box, three interleaved rounds (round 5, before them: no gain)
+#endif
+#ifndef TPT_CONN_STEAL_CAP
+#define TPT_CONN_STEAL_CAP 0  // steals per query round (0: no cap; round 6, bunny BDPT 256 spp: cap 64 / 256 / 1024 /
+                              // none 600.5 / 557-559 / 561 / 559 ms same-box; the walks are finite, so stealing ends)
 #endif
 TPT_D bool walk4_shadow_steal(const DScene& s, int root, bool need, Ray r, double thr, int cl) {
     QScratch* qs = wave_qs(s);
@@ -732,7 +744,17 @@ TPT_D bool walk4_shadow_steal(const DScene& s, int root, bool need, Ray r, doubl
         const uint64_t vm = __ballot(job && sp > sb);
         const uint64_t im = __ballot(!job);
         int m = __popcll(im) < __popcll(vm) ? __popcll(im) : __popcll(vm);
-        if (m > 64 - jobs) m = 64 - jobs;  // a bounded number of steals per query
+#if TPT_CONN_STEAL_CAP > 0
+        {
+            int cap = TPT_CONN_STEAL_CAP;
+#if TPT_STEAL_CAP_OPAQUE
+            asm volatile("" : "+s"(cap));
+#endif
+            if (m > cap - jobs) m = cap - jobs;  // a bounded number of steals per query
+        }
+#else
+        (void)jobs;
+#endif
         if (m > 0) {
             if (job && sp > sb) {
                 const int k = mbcnt64(vm);
