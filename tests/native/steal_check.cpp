@@ -1,4 +1,5 @@
-// Host check of the gen kernel's stealing walk (VERDICT r5 Next #2, ADVICE r5 tie fixture).
+// Host check of the gen kernel's stealing walk (VERDICT r5 Next #2, ADVICE r5 tie fixture)
+// and of connect's stealing shadow walk (round 6, TPT_CONN_STEAL).
 //
 // The shipped device function itself -- tpt_bdpt.h's walk4_steal, with its mailbox, job
 // list and per-ray merge -- runs here unmodified on an emulated 64-lane wavefront
@@ -352,6 +353,60 @@ static Tally check(HostDev& h, int waves, unsigned seed, const float* room_lo, c
     return t;
 }
 
+// ---- connect's stealing shadow walk (walk4_shadow_steal, tpt_device.h; TPT_CONN_STEAL) ----
+// Every lane: a segment from its origin along its ray to a point at a random length, with
+// ShadowCheck's threshold |x - o|^2 - 1 (shadow_ray).  The stealing walk's answer (uncapped
+// by default, TPT_CONN_STEAL_CAP) must equal the per-lane threaded any-hit walk
+// (walk_group_shadow: the connect path without stealing) and the closest-hit criterion of
+// the DFS fold (walk_group_closest's hit at |hit - o|^2 < thr: Scene::ShadowCheck).
+struct ShTally {
+    long rays = 0, need = 0, shadowed = 0, bad_steal = 0, bad_any = 0;
+};
+static ShTally check_shadow(HostDev& h, int waves, unsigned seed, const float* lo, const float* hi) {
+    ShTally t;
+    std::mt19937 g(seed);
+    std::uniform_real_distribution<float> u(0.0f, 1.0f);
+    const DScene& s = h.ds;
+    const DNode gn = h.hs.groups[h.gw];
+    const int walk_counts[] = {1, 3, 8, 19, 24, 40, 64};
+    for (int w = 0; w < waves; ++w) {
+        const std::vector<Job> js = make_wave(g, h, walk_counts[w % 7], w % 4, lo, hi);
+        float len[64];
+        for (int l = 0; l < 64; ++l) len[l] = 20.0f + 600.0f * u(g);
+        bool steal[64], any[64], dfs[64], need[64];
+        wemu::run([&](int lane) {
+            const Job& j = js[lane];
+            const V3 x = j.o + mul(j.d, len[lane]);
+            const double thr = dot3(j.o - x, j.o - x) - 1.0f;
+            const Ray r = make_ray(j.o, normalized(x - j.o));
+            const bool nd =
+                slab_hit_finite(gn.bmin[0], gn.bmin[1], gn.bmin[2], gn.bmax[0], gn.bmax[1], gn.bmax[2], r);
+            need[lane] = nd;
+            steal[lane] = walk4_shadow_steal(s, -2 - gn.b, nd, r, thr, j.cl);
+            any[lane] = nd && walk_group_shadow(s, gn.a, r, r.o, thr, j.cl);
+            Hit b;
+            b.prim = -1;
+            b.dist = 0.0;
+            if (nd) walk_group_closest(s, gn.a, r, j.cl, b);
+            bool sh = false;
+            if (b.prim >= 0) {
+                const V3 hx = r.o + mul(r.d, (float)b.dist);
+                sh = dot3(hx - r.o, hx - r.o) < thr;
+            }
+            dfs[lane] = sh;
+        });
+        for (int l = 0; l < 64; ++l) {
+            ++t.rays;
+            if (!need[l]) continue;
+            ++t.need;
+            if (dfs[l]) ++t.shadowed;
+            if (steal[l] != dfs[l]) ++t.bad_steal;
+            if (any[l] != dfs[l]) ++t.bad_any;
+        }
+    }
+    return t;
+}
+
 // Ties: a grid mesh whose every triangle appears twice (the same vertices in the same
 // order), so both copies give the same f64 distance; the reference keeps the copy its DFS
 // visits first.  The desc owns its arrays.
@@ -414,6 +469,10 @@ int main(int argc, char** argv) {
                     "per-lane walk4 != DFS: %ld (%llu collectives)\n",
                     t.waves, t.rays, t.need, t.hits, t.bad_steal, t.bad_seq, t.coll);
         ok = ok && t.bad_steal == 0 && t.bad_seq == 0 && t.hits > 1000;
+        const ShTally sh = check_shadow(h, waves, 4321u, lo, hi);
+        std::printf("bunny shadow: %ld rays, %ld walked the group, %ld shadowed; stealing shadow walk != DFS: %ld, "
+                    "per-lane any-hit walk != DFS: %ld\n", sh.rays, sh.need, sh.shadowed, sh.bad_steal, sh.bad_any);
+        ok = ok && sh.bad_steal == 0 && sh.bad_any == 0 && sh.shadowed > 1000 && sh.need - sh.shadowed > 1000;
         for (int f = 1; f <= 2; ++f) {
             Tally a = check(h, waves, 1234u, lo, hi, f);
             std::printf("bunny, LDS atomic-minimum merge form %d (not shipped): %ld of %ld hits differ from DFS (%.2f %%)\n",
@@ -454,6 +513,10 @@ int main(int argc, char** argv) {
                     "two-leaf ties); stealing walk != DFS: %ld, per-lane walk4 != DFS: %ld\n",
                     t.waves, t.rays, t.need, t.hits, ties, checked, t.bad_steal, t.bad_seq);
         ok = ok && t.bad_steal == 0 && t.bad_seq == 0 && t.hits > 1000 && ties > checked / 2;
+        const ShTally sh = check_shadow(h, waves / 2, 4321u, lo, hi);
+        std::printf("ties shadow: %ld rays, %ld walked the group, %ld shadowed; stealing shadow walk != DFS: %ld, "
+                    "per-lane any-hit walk != DFS: %ld\n", sh.rays, sh.need, sh.shadowed, sh.bad_steal, sh.bad_any);
+        ok = ok && sh.bad_steal == 0 && sh.bad_any == 0 && sh.shadowed > 100;
         for (int f = 1; f <= 2; ++f) {
             Tally a = check(h, waves / 2, 99u, lo, hi, f);
             std::printf("ties, LDS atomic-minimum merge form %d (not shipped): %ld of %ld hits differ from DFS\n", f - 1,
